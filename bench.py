@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpixels/s at 1920x1080, 2000 geodesic steps, default
+scene (BASELINE.json `metric`, config 3), curved mode, noise mask off.
+
+One step = one full frame: every rank renders its block-cyclic share of the
+frame's rows (8-row blocks, block b -> rank b % N) with the gfx950 kernel,
+then the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl").
+`value` = frame pixels x K / (max over ranks of the timed span) — strong
+scaling (the frame is fixed, the GPUs share it).
+
+Inputs are resident in HBM before timing (scene, textures, step table).
+Also reported: the kernel's roofline (algorithmic FLOP/s from the executed
+step count, SURVEY §8d cost model, HIP events on the render stream) and the
+reference's CPU press-R geodesic loop swept over a sample of the frame's
+pixels on this host (cpu_baseline; oracle restatement, "port").
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+# algorithmic cost per executed chord step in the default
+# scene (integrator 71 + black hole 17 + six objects, all-miss) and per pixel.
+FLOP_PER_STEP = 360.0
+FLOP_PER_PIXEL = 150.0
+# MI355X_MICROARCH.md: FP32 vector peak (packed FMA) and HBM3E peak.
+PEAK_FP32_TFLOPS = 157.3
+PEAK_FP32_UNPACKED_TFLOPS = 78.6
+PEAK_HBM_GBS = 8000.0
+BLOCK_ROWS = 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import srpkg
+
+    pkg = srpkg.load_package()
+    abi, sc = pkg.abi, pkg.scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    W, H, N = args.width, args.height, args.max_steps
+
+    # ---- inputs resident in HBM ---------------------------------------------------
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    r = pkg.Renderer(local)
+    r.set_scene(scene)
+    r.set_background(sc.skybox(2048, 1024))
+    arr, _, _ = sc.default_texture_array()
+    r.set_texture_array(arr)
+    r.set_culling(not args.no_cull)
+
+    nblocks = (H + BLOCK_ROWS - 1) // BLOCK_ROWS
+    my_blocks = len(range(rank, nblocks, world))
+    tile_rows = ((nblocks + world - 1) // world) * BLOCK_ROWS  # equal-size tiles for the gather
+    tile = torch.zeros((tile_rows, W, 4), dtype=torch.uint8, device=dev)
+    gathered = None
+    if distributed and rank == 0:
+        gathered = [torch.empty_like(tile) for _ in range(world)]
+    stream = torch.cuda.current_stream(dev)
+
+    def render_tile():
+        r.render_blocks(cam, params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+
+    def step():
+        render_tile()
+        if distributed:
+            dist.gather(tile, gathered if rank == 0 else None, dst=0)
+
+    # executed steps of this rank's rows (untimed; the debug variant of the kernel)
+    rows_mine = []
+    for b in range(rank, nblocks, world):
+        rows_mine.extend(range(b * BLOCK_ROWS, min(H, (b + 1) * BLOCK_ROWS)))
+    _, _, steps_full = r.render_debug(cam, params, W, H)
+    torch.cuda.synchronize(dev)
+    sigma_steps_frame = int(steps_full.sum().item())
+    sigma_steps_mine = int(steps_full[rows_mine].sum().item())
+    del steps_full
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # kernel-only timing with HIP events on the render stream (separate loop
+    # so the gather does not sit between the events)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        render_tile()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        k = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(k, op=dist.ReduceOp.MAX)
+        kernel_ms_max = float(k.item())
+    else:
+        kernel_ms_max = kernel_ms
+
+    ms_per_step = elapsed * 1e3 / args.steps
+    mpix_s = W * H * args.steps / elapsed / 1e6
+
+    if rank == 0:
+        # roofline of the dominant (only) kernel, on rank 0's launch
+        flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL
+        achieved_tflops = flop / (kernel_ms * 1e-3) / 1e12
+        hbm_bytes = len(rows_mine) * W * 4  # compulsory RGBA8 store; textures stay cache resident
+        traffic = None
+        tj = Path(args.traffic_json)
+        if tj.exists():
+            try:
+                rec = json.loads(tj.read_text())
+                if rec.get("width") == W and rec.get("height") == H and rec.get("max_steps") == N and world == 1:
+                    traffic = rec.get("hbm_bytes_per_launch")
+            except Exception:  # noqa: BLE001
+                traffic = None
+        roofline = {
+            "bound": "valu",
+            "achieved": round(achieved_tflops, 3),
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic,
+            "frac_unpacked_peak": round(achieved_tflops / PEAK_FP32_UNPACKED_TFLOPS, 4),
+            "kernel_ms": round(kernel_ms, 4),
+            "flop_per_launch": flop,
+            "steps_per_launch": sigma_steps_mine,
+            "mean_steps_per_pixel": round(sigma_steps_frame / (W * H), 2),
+            "hbm": {
+                "achieved": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 3),
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
+                "algorithmic_bytes": hbm_bytes,
+            },
+        }
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            cpu = cpu_baseline(cam, W, H, N, args.cpu_sample_rows)
+        line = {
+            "metric": "Mpixels/s at 1920x1080, 2000 geodesic steps; 1/2/4/8 MI355X",
+            "value": round(mpix_s, 3),
+            "unit": "Mpixels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (default scene of src/main.cpp:222-268, procedural stand-in textures)",
+            "config": {
+                "workload": f"{W}x{H} curved-mode frame, {N} geodesic steps, default scene, percent_black off",
+                "width": W,
+                "height": H,
+                "max_steps": N,
+                "tiling": f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), RCCL gather to rank 0",
+                "culling": not args.no_cull,
+                "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
+            },
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    r.close()
+
+
+def cpu_baseline(cam, W, H, N, sample_rows):
+    """The reference's press-R CPU geodesic (src/main.cpp:73-124) swept over
+    a bounded sample of the frame's pixels, all host cores (oracle port)."""
+    import srpkg
+
+    oracle = srpkg.load_oracle()
+    threads = min(16, os.cpu_count() or 1)
+    if sample_rows <= 0:
+        # calibrate: time 8 rows, size the sample to ~10 s of work
+        t = time.perf_counter()
+        oracle.pressr_sweep(cam, W, H, N, 2, H // 2 - 4, H // 2 + 4, threads)
+        dt = max(time.perf_counter() - t, 1e-3)
+        sample_rows = int(min(H, max(8, 8 * 10.0 / dt)))
+    # evenly spread bands: rows [y0, y0 + n) around the frame centre
+    y0 = max(0, H // 2 - sample_rows // 2)
+    y1 = min(H, y0 + sample_rows)
+    t = time.perf_counter()
+    pts = oracle.pressr_sweep(cam, W, H, N, 2, y0, y1, threads)
+    dt = time.perf_counter() - t
+    px = (y1 - y0) * W
+    return {
+        "value": round(px / dt / 1e6, 4),
+        "unit": "Mpixels/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"press-R loop (src/main.cpp:73-124) over rows [{y0},{y1}) x {W} px of the {W}x{H} frame, "
+                  f"{N} steps, {pts} points, {dt:.2f} s, -O2",
+    }
+
+
+if __name__ == "__main__":
+    main()

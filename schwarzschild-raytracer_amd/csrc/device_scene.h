@@ -1,0 +1,93 @@
+// device_scene.h — the launch-invariant scene image the kernel reads with
+// wave-uniform (scalar) loads. Built once per sr_set_scene / sr_set_test_ray
+// by the host packer (sr_api.cpp) from the GLSL-shaped sr_scene; every derived
+// value (box faces, test-ray frames, bounding spheres) is computed on the host
+// with the same float operations the shader performs per call, so the kernel's
+// results are bit-identical to evaluating them per step.
+#ifndef SR_DEVICE_SCENE_H
+#define SR_DEVICE_SCENE_H
+
+#include <stdint.h>
+
+#include "sr/sr.h"
+
+#define SR_OBJ_FLOATS 120
+
+// Record float layout (f[]):
+//   [0..2] pos   [3..11] axes (column-major)
+//   sphere   : [12] radius
+//   plane*   : [12,13] texture_offset [14] repeat_texture [15,16] texture_size
+//   disk     : plane* + [17] radius
+//   hollow   : plane* + [17] inner_radius [18] outer_radius
+//   rectangle: plane* + [17] width [18] height
+//   cylinder : [12] height [13] radius
+//   box      : [12] width [13] depth [14] height, then 6 faces (bot, top,
+//              front, back, left, right; frag:649) at 16 + 14*face:
+//              pos[3] c0[3] c1[3] c2[3] width height
+#define SR_F_POS 0
+#define SR_F_AXES 3
+#define SR_F_P0 12
+#define SR_F_BOX_FACE0 16
+#define SR_F_FACE_STRIDE 14
+
+typedef struct {
+    int32_t type;
+    int32_t index;
+    int32_t material_index;
+    int32_t cull;    // 1: bounding sphere below is valid for segment culling
+    float bc[3];     // bounding-sphere centre
+    float br;        // bounding-sphere radius (static margin included)
+    float f[SR_OBJ_FLOATS];
+} sr_dev_obj;  // 512 B
+
+// One test-ray cylinder: pos[3] axes[9] height radius, padded to 16 floats.
+#define SR_SEG_FLOATS 16
+
+typedef struct {
+    int32_t num_objects;
+    int32_t num_lights;
+    int32_t tr_visible;
+    int32_t tr_num_segments;  // num_test_ray_curved_points - 1 (>= 0)
+    float tr_radius;
+    float tr_extended_length;
+    float pad0[2];
+    float tr_curved_color[4];
+    float tr_flat_color[4];
+    float tr_flat[SR_SEG_FLOATS];  // flat test-ray cylinder
+    sr_dev_obj objs[SR_MAX_OBJECTS];
+    sr_material materials[SR_MAX_MATERIALS];
+    sr_light lights[SR_MAX_LIGHTS];
+    sr_plane planes[SR_MAX_PLANES];
+    float texture_sizes[SR_MAX_TEXTURES][2];
+    float max_texture_size[2];
+} sr_dev_scene;
+
+// Per-launch constants (kernel argument, scalar-loaded).
+typedef struct {
+    float cam_pos[3];
+    float cam_axes[9];
+    float ray_forward;  // 1 / tan(fov/360*PI), computed once on the host (frag:859)
+    float max_angle;    // 2 * max_revolutions * PI (frag:860)
+    float res_x, res_y; // resolution uniform == frame size
+    float u_f;
+    float uf_radius;    // 1 / u_f (frag:893)
+    float percent_black;
+    float curved_percentage;
+    int32_t max_steps;
+    int32_t raytrace_type;
+    int32_t crosshair;
+    int32_t filter_mode;
+    int32_t cull;       // segment culling on/off (off = the reference's exhaustive loop)
+    int32_t width, height;
+    // output row mapping: output row k renders frame row
+    //   y = row_base + (k / block_rows) * block_stride + (k % block_rows)
+    int32_t nrows;
+    int32_t row_base;
+    int32_t block_rows;
+    int32_t block_stride;
+    // textures (RGBA8 texels)
+    int32_t bg_w, bg_h;
+    int32_t arr_w, arr_h, arr_layers;
+} sr_dev_frame;
+
+#endif

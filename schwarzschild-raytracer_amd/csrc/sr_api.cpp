@@ -1,0 +1,526 @@
+// sr_api.cpp — the C-ABI of include/sr/sr.h: device context, texture and
+// scene uploads, launch-invariant precomputation, and kernel dispatch.
+// Replaces the reference's GL program interface: the draw call of
+// src/main.cpp:318-319 becomes sr_render, the loadShader uniform uploads
+// become sr_set_scene / sr_set_test_ray snapshots.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "device_scene.h"
+#include "sr/sr.h"
+
+extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
+                                         const uint32_t* bg, const uint32_t* arr, const sr_dev_frame* fr,
+                                         uint8_t* out, size_t pitch, float* dbg_rgba, int32_t* dbg_steps,
+                                         hipStream_t stream);
+
+namespace {
+
+constexpr float kPi = 3.1415926535f;  // frag:10
+
+struct Table {
+    float4* dev = nullptr;
+    int steps = 0;
+};
+
+}  // namespace
+
+struct sr_ctx {
+    int device = 0;
+    sr_dev_scene* d_scene = nullptr;
+    float* d_segs = nullptr;
+    uint32_t* d_bg = nullptr;
+    int bg_w = 0, bg_h = 0;
+    uint32_t* d_arr = nullptr;
+    int arr_w = 0, arr_h = 0, arr_layers = 0;
+    bool scene_set = false;
+    bool cull = true;
+    sr_dev_scene h_scene;
+    std::map<std::pair<int, int>, Table> tables;  // (max_steps, max_revolutions) -> table
+};
+
+namespace {
+
+// ---- small float helpers with the kernel's evaluation order ----------------
+struct V3 {
+    float x, y, z;
+};
+inline V3 v3(float x, float y, float z) { return {x, y, z}; }
+inline V3 ld(const float* p) { return {p[0], p[1], p[2]}; }
+inline void st(float* p, V3 v) {
+    p[0] = v.x;
+    p[1] = v.y;
+    p[2] = v.z;
+}
+inline V3 add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 scl(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+inline V3 neg(V3 a) { return {-a.x, -a.y, -a.z}; }
+inline float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline float len(V3 a) { return std::sqrt(dot(a, a)); }
+inline V3 nrm(V3 a) { return scl(a, 1.0f / std::sqrt(dot(a, a))); }
+// columns c0, c1, c2: (c0*v.x + c1*v.y) + c2*v.z
+inline V3 mv(V3 c0, V3 c1, V3 c2, V3 v) { return add(add(scl(c0, v.x), scl(c1, v.y)), scl(c2, v.z)); }
+inline float l1norm(V3 a) { return std::fabs(a.x) + std::fabs(a.y) + std::fabs(a.z); }
+
+bool orthonormal(V3 a, V3 b, V3 c) {
+    const float tol = 1e-5f;
+    return std::fabs(dot(a, a) - 1.f) < tol && std::fabs(dot(b, b) - 1.f) < tol &&
+           std::fabs(dot(c, c) - 1.f) < tol && std::fabs(dot(a, b)) < tol &&
+           std::fabs(dot(a, c)) < tol && std::fabs(dot(b, c)) < tol;
+}
+
+void set_bound(sr_dev_obj& o, V3 c, float R) {
+    if (!std::isfinite(R) || !std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z)) {
+        o.cull = 0;
+        return;
+    }
+    st(o.bc, c);
+    o.br = R + 1e-4f * (1.f + l1norm(c) + R);
+    o.cull = 1;
+}
+
+void put_transform(float* f, const sr_transform& t) {
+    std::memcpy(f + SR_F_POS, t.pos, 3 * sizeof(float));
+    std::memcpy(f + SR_F_AXES, t.axes, 9 * sizeof(float));
+}
+void put_plane(float* f, const sr_plane& p) {
+    put_transform(f, p.transform);
+    f[12] = p.texture_offset[0];
+    f[13] = p.texture_offset[1];
+    f[14] = (float)p.repeat_texture;
+    f[15] = p.texture_size[0];
+    f[16] = p.texture_size[1];
+}
+
+// One rectangle face of a box (frag:587-647): pos, columns, width, height.
+void put_face(float* g, V3 pos, V3 c0, V3 c1, V3 c2, float w, float h) {
+    st(g, pos);
+    st(g + 3, c0);
+    st(g + 6, c1);
+    st(g + 9, c2);
+    g[12] = w;
+    g[13] = h;
+}
+
+int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
+    const sr_object& so = s.objects[i];
+    std::memset(&o, 0, sizeof o);
+    o.type = so.type;
+    o.index = so.index;
+    o.material_index = so.material_index;
+    if (so.material_index < 0 || so.material_index >= SR_MAX_MATERIALS) return SR_E_CAPACITY;
+    const int k = so.index;
+    float* f = o.f;
+    switch (so.type) {
+    case SR_OBJECT_SPHERE: {
+        if (k < 0 || k >= SR_MAX_SPHERES) return SR_E_CAPACITY;
+        put_transform(f, s.spheres[k].transform);
+        f[SR_F_P0] = s.spheres[k].radius;
+        o.cull = 0;  // the sphere test is as cheap as the cull test
+        return SR_OK;
+    }
+    case SR_OBJECT_PLANE:
+        if (k < 0 || k >= SR_MAX_PLANES) return SR_E_CAPACITY;
+        put_plane(f, s.planes[k]);
+        o.cull = 0;  // unbounded
+        return SR_OK;
+    case SR_OBJECT_DISK: {
+        if (k < 0 || k >= SR_MAX_DISKS) return SR_E_CAPACITY;
+        put_plane(f, s.disks[k].plane);
+        f[17] = s.disks[k].radius;
+        set_bound(o, ld(f), std::fabs(f[17]));
+        return SR_OK;
+    }
+    case SR_OBJECT_HOLLOW_DISK: {
+        if (k < 0 || k >= SR_MAX_HOLLOW_DISKS) return SR_E_CAPACITY;
+        put_plane(f, s.hollow_disks[k].plane);
+        f[17] = s.hollow_disks[k].inner_radius;
+        f[18] = s.hollow_disks[k].outer_radius;
+        set_bound(o, ld(f), std::fabs(f[18]));
+        return SR_OK;
+    }
+    case SR_OBJECT_CYLINDER: {
+        if (k < 0 || k >= SR_MAX_CYLINDERS) return SR_E_CAPACITY;
+        put_transform(f, s.cylinders[k].transform);
+        float h = s.cylinders[k].height, r = s.cylinders[k].radius;
+        f[SR_F_P0] = h;
+        f[SR_F_P0 + 1] = r;
+        V3 a0 = ld(f + 3), a1 = ld(f + 6), a2 = ld(f + 9);
+        if (orthonormal(a0, a1, a2) && h >= 0.f && r > 0.f) {
+            double hh = 0.5 * h;
+            set_bound(o, add(ld(f), scl(a1, (float)hh)), (float)std::sqrt((double)r * r + hh * hh));
+        }
+        return SR_OK;
+    }
+    case SR_OBJECT_RECTANGLE: {
+        if (k < 0 || k >= SR_MAX_RECTANGLES) return SR_E_CAPACITY;
+        put_plane(f, s.rectangles[k].plane);
+        float w = s.rectangles[k].width, h = s.rectangles[k].height;
+        f[17] = w;
+        f[18] = h;
+        V3 a0 = ld(f + 3), a1 = ld(f + 6), a2 = ld(f + 9);
+        if (orthonormal(a0, a1, a2) && w >= 0.f && h >= 0.f) {
+            V3 c = add(ld(f), add(scl(a0, 0.5f * w), scl(a2, 0.5f * h)));
+            set_bound(o, c, (float)std::sqrt(0.25 * w * w + 0.25 * h * h));
+        }
+        return SR_OK;
+    }
+    case SR_OBJECT_BOX: {
+        if (k < 0 || k >= SR_MAX_BOXES) return SR_E_CAPACITY;
+        const sr_box& b = s.boxes[k];
+        put_transform(f, b.transform);
+        f[12] = b.width;
+        f[13] = b.depth;
+        f[14] = b.height;
+        V3 p = ld(b.transform.pos);
+        V3 a0 = ld(b.transform.axes), a1 = ld(b.transform.axes + 3), a2 = ld(b.transform.axes + 6);
+        float* F = f + SR_F_BOX_FACE0;
+        const int S = SR_F_FACE_STRIDE;
+        // frag:587-647, order bot, top, front, back, left, right (frag:649)
+        put_face(F + 0 * S, add(p, scl(a2, b.depth)), a0, neg(a1), neg(a2), b.width, b.depth);
+        put_face(F + 1 * S, add(p, scl(a1, b.height)), a0, a1, a2, b.width, b.depth);
+        put_face(F + 2 * S, add(p, mv(a0, a1, a2, v3(0.f, b.height, b.depth))), a0, a2, neg(a1), b.width,
+                 b.height);
+        put_face(F + 3 * S, add(p, mv(a0, a1, a2, v3(b.width, b.height, 0.f))), neg(a0), neg(a2), neg(a1),
+                 b.width, b.height);
+        put_face(F + 4 * S, add(p, scl(a1, b.height)), a2, neg(a0), neg(a1), b.depth, b.height);
+        put_face(F + 5 * S, add(p, mv(a0, a1, a2, v3(b.width, b.height, b.depth))), neg(a2), a0, neg(a1),
+                 b.depth, b.height);
+        if (orthonormal(a0, a1, a2) && b.width >= 0.f && b.depth >= 0.f && b.height >= 0.f) {
+            V3 c = add(p, mv(a0, a1, a2, v3(0.5f * b.width, 0.5f * b.height, 0.5f * b.depth)));
+            double R = 0.5 * std::sqrt((double)b.width * b.width + (double)b.height * b.height +
+                                       (double)b.depth * b.depth);
+            set_bound(o, c, (float)R);
+        }
+        return SR_OK;
+    }
+    default:
+        return SR_E_INVALID;
+    }
+}
+
+// gram_schmidt(mat3(d.xzy, d, d.zxy)), frag:739-753, 764, 789
+void test_ray_frame(V3 d, float* axes9) {
+    V3 m0 = v3(d.x, d.z, d.y), m1 = d, m2 = v3(d.z, d.x, d.y);
+    auto project = [](V3 v, V3 t) { return scl(t, dot(v, t) / dot(t, t)); };
+    m0 = sub(m0, project(m0, m1));
+    m2 = sub(sub(m2, project(m2, m1)), project(m2, m0));
+    st(axes9, nrm(m0));
+    st(axes9 + 3, nrm(m1));
+    st(axes9 + 6, nrm(m2));
+}
+
+inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
+
+int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
+    auto key = std::make_pair(max_steps, max_revs);
+    auto it = ctx->tables.find(key);
+    if (it != ctx->tables.end()) {
+        *out = it->second.dev;
+        return SR_OK;
+    }
+    // frag:860, 914-915, 925: the angle sequence depends only on the step index
+    const float max_angle = 2.0f * (float)max_revs * kPi;
+    std::vector<float4> h((size_t)(max_steps > 0 ? max_steps : 1));
+    float phi = 0.0f;
+    for (int i = 0; i < max_steps; i++) {
+        float step = (max_angle - phi) / (float)(max_steps - i);
+        phi += step;
+        h[i] = make_float4(step, phi, (float)std::cos((double)phi), (float)std::sin((double)phi));
+    }
+    Table t;
+    t.steps = max_steps;
+    if (!hip_ok(hipMalloc(&t.dev, h.size() * sizeof(float4)))) return SR_E_NOMEM;
+    if (!hip_ok(hipMemcpy(t.dev, h.data(), h.size() * sizeof(float4), hipMemcpyHostToDevice))) {
+        (void)hipFree(t.dev);
+        return SR_E_HIP;
+    }
+    ctx->tables[key] = t;
+    *out = t.dev;
+    return SR_OK;
+}
+
+int upload_rgba(const uint8_t* px, int w, int h, int layers, int ch, uint32_t** dev) {
+    size_t n = (size_t)w * h * layers;
+    std::vector<uint32_t> rgba(n);
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t* p = px + i * ch;
+        uint32_t a = ch == 4 ? p[3] : 255u;  // GL_RGB reads alpha 1
+        rgba[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (a << 24);
+    }
+    if (*dev) {
+        (void)hipFree(*dev);
+        *dev = nullptr;
+    }
+    if (!hip_ok(hipMalloc(dev, n * sizeof(uint32_t)))) return SR_E_NOMEM;
+    if (!hip_ok(hipMemcpy(*dev, rgba.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice))) return SR_E_HIP;
+    return SR_OK;
+}
+
+int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
+    if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
+    if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
+    if (p->filter_mode != SR_FILTER_LERP && p->filter_mode != SR_FILTER_WEIGHTED) return SR_E_INVALID;
+    if (p->max_steps < 0 || p->max_steps > (1 << 24)) return SR_E_INVALID;
+    std::memset(&fr, 0, sizeof fr);
+    std::memcpy(fr.cam_pos, cam->transform.pos, sizeof fr.cam_pos);
+    std::memcpy(fr.cam_axes, cam->transform.axes, sizeof fr.cam_axes);
+    // frag:859-860 (launch invariants, same float ops)
+    fr.ray_forward = 1.0f / (float)std::tan((double)(cam->fov / 360.0f * kPi));
+    fr.max_angle = 2.0f * (float)p->max_revolutions * kPi;
+    fr.res_x = (float)width;
+    fr.res_y = (float)height;
+    fr.u_f = p->u_f;
+    fr.uf_radius = 1.0f / p->u_f;
+    fr.percent_black = p->percent_black;
+    fr.curved_percentage = p->curved_percentage;
+    fr.max_steps = p->max_steps;
+    fr.raytrace_type = p->raytrace_type;
+    fr.crosshair = p->crosshair;
+    fr.filter_mode = p->filter_mode;
+    fr.cull = ctx->cull ? 1 : 0;
+    fr.width = width;
+    fr.height = height;
+    fr.bg_w = ctx->bg_w;
+    fr.bg_h = ctx->bg_h;
+    fr.arr_w = ctx->arr_w;
+    fr.arr_h = ctx->arr_h;
+    fr.arr_layers = ctx->arr_layers;
+    return SR_OK;
+}
+
+int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width, int height, int nrows,
+           int row_base, int block_rows, int block_stride, uint8_t* out, size_t pitch, float* dbg_rgba,
+           int32_t* dbg_steps, sr_stream stream) {
+    if (!ctx) return SR_E_INVALID;
+    if (!ctx->scene_set) return SR_E_NOT_READY;
+    sr_dev_frame fr;
+    int rc = build_frame(ctx, cam, params, width, height, fr);
+    if (rc != SR_OK) return rc;
+    if (nrows < 0 || block_rows <= 0) return SR_E_INVALID;
+    if (out && pitch < (size_t)width * 4) return SR_E_INVALID;
+    fr.nrows = nrows;
+    fr.row_base = row_base;
+    fr.block_rows = block_rows;
+    fr.block_stride = block_stride;
+    if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
+    const float4* tbl = nullptr;
+    rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
+    if (rc != SR_OK) return rc;
+    hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, &fr, out, pitch,
+                                      dbg_rgba, dbg_steps, reinterpret_cast<hipStream_t>(stream));
+    return hip_ok(e) ? SR_OK : SR_E_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* sr_version(void) { return "schwarzschild-mi355x 0.1 (gfx950)"; }
+
+const char* sr_status_string(int s) {
+    switch (s) {
+    case SR_OK: return "ok";
+    case SR_E_INVALID: return "invalid argument";
+    case SR_E_CAPACITY: return "capacity exceeded";
+    case SR_E_HIP: return "HIP runtime error";
+    case SR_E_NOMEM: return "out of memory";
+    case SR_E_NOT_READY: return "scene not set";
+    case SR_E_NO_DEVICE: return "no HIP device";
+    default: return "unknown status";
+    }
+}
+
+int sr_create(sr_ctx** out, int hip_device) {
+    if (!out) return SR_E_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (!hip_ok(hipGetDeviceCount(&n)) || n <= 0) return SR_E_NO_DEVICE;
+    if (hip_device < 0 || hip_device >= n) return SR_E_NO_DEVICE;
+    if (!hip_ok(hipSetDevice(hip_device))) return SR_E_HIP;
+    sr_ctx* c = new (std::nothrow) sr_ctx();
+    if (!c) return SR_E_NOMEM;
+    c->device = hip_device;
+    std::memset(&c->h_scene, 0, sizeof c->h_scene);
+    if (!hip_ok(hipMalloc(&c->d_scene, sizeof(sr_dev_scene))) ||
+        !hip_ok(hipMalloc(&c->d_segs, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float)))) {
+        sr_destroy(c);
+        return SR_E_NOMEM;
+    }
+    if (!hip_ok(hipMemset(c->d_scene, 0, sizeof(sr_dev_scene))) ||
+        !hip_ok(hipMemset(c->d_segs, 0, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float)))) {
+        sr_destroy(c);
+        return SR_E_HIP;
+    }
+    sr_test_ray tr;
+    sr_test_ray_default(&tr);
+    int rc = sr_set_test_ray(c, &tr);
+    if (rc != SR_OK) {
+        sr_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return SR_OK;
+}
+
+void sr_destroy(sr_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->d_scene) (void)hipFree(c->d_scene);
+    if (c->d_segs) (void)hipFree(c->d_segs);
+    if (c->d_bg) (void)hipFree(c->d_bg);
+    if (c->d_arr) (void)hipFree(c->d_arr);
+    for (auto& kv : c->tables) (void)hipFree(kv.second.dev);
+    delete c;
+}
+
+int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {
+    if (!c || !px || w <= 0 || h <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
+    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    int rc = upload_rgba(px, w, h, 1, ch, &c->d_bg);
+    if (rc != SR_OK) {
+        c->bg_w = c->bg_h = 0;
+        return rc;
+    }
+    c->bg_w = w;
+    c->bg_h = h;
+    return SR_OK;
+}
+
+int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers, int ch) {
+    if (!c || !px || w <= 0 || h <= 0 || layers <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
+    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    int rc = upload_rgba(px, w, h, layers, ch, &c->d_arr);
+    if (rc != SR_OK) {
+        c->arr_w = c->arr_h = c->arr_layers = 0;
+        return rc;
+    }
+    c->arr_w = w;
+    c->arr_h = h;
+    c->arr_layers = layers;
+    return SR_OK;
+}
+
+int sr_set_scene(sr_ctx* c, const sr_scene* s) {
+    if (!c || !s) return SR_E_INVALID;
+    if (s->num_objects < 0 || s->num_lights < 0) return SR_E_INVALID;
+    if (s->num_objects > SR_MAX_OBJECTS || s->num_lights > SR_MAX_LIGHTS) return SR_E_CAPACITY;
+    sr_dev_scene d = c->h_scene;  // keeps the test-ray part
+    d.num_objects = s->num_objects;
+    d.num_lights = s->num_lights;
+    std::memset(d.objs, 0, sizeof d.objs);
+    for (int i = 0; i < s->num_objects; i++) {
+        int rc = pack_object(*s, i, d.objs[i]);
+        if (rc != SR_OK) return rc;
+    }
+    std::memcpy(d.materials, s->materials, sizeof d.materials);
+    std::memcpy(d.lights, s->lights, sizeof d.lights);
+    std::memcpy(d.planes, s->planes, sizeof d.planes);
+    std::memcpy(d.texture_sizes, s->texture_sizes, sizeof d.texture_sizes);
+    std::memcpy(d.max_texture_size, s->max_texture_size, sizeof d.max_texture_size);
+    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
+    c->h_scene = d;
+    c->scene_set = true;
+    return SR_OK;
+}
+
+int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
+    if (!c || !t) return SR_E_INVALID;
+    if (t->num_curved_points < 0 || t->num_curved_points > SR_MAX_POINTS) return SR_E_CAPACITY;
+    sr_dev_scene d = c->h_scene;
+    d.tr_visible = t->visible ? 1 : 0;
+    d.tr_radius = t->radius;
+    d.tr_extended_length = t->extended_length;
+    std::memcpy(d.tr_curved_color, t->curved_color, sizeof d.tr_curved_color);
+    std::memcpy(d.tr_flat_color, t->flat_color, sizeof d.tr_flat_color);
+    std::memset(d.tr_flat, 0, sizeof d.tr_flat);
+    st(d.tr_flat, ld(t->flat_origin));
+    test_ray_frame(ld(t->flat_dir), d.tr_flat + 3);
+    d.tr_flat[12] = t->extended_length;
+    d.tr_flat[13] = t->radius;
+    const int n = t->num_curved_points;
+    const int nseg = n >= 2 ? n - 1 : 0;
+    std::vector<float> segs((size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS, 0.f);
+    for (int i = 0; i < nseg; i++) {  // frag:777-793
+        float* g = segs.data() + (size_t)i * SR_SEG_FLOATS;
+        V3 pi = ld(t->curved_points[i]);
+        V3 diff = sub(ld(t->curved_points[i + 1]), pi);
+        float h = len(diff);
+        if (i == n - 2 && len(ld(t->curved_points[n - 1])) < 1.0f) h = t->extended_length;
+        st(g, pi);
+        test_ray_frame(diff, g + 3);
+        g[12] = h;
+        g[13] = t->radius;
+    }
+    d.tr_num_segments = nseg;
+    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipMemcpy(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice)))
+        return SR_E_HIP;
+    if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
+    c->h_scene = d;
+    return SR_OK;
+}
+
+int sr_render(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, int height, int row_begin,
+              int row_end, uint8_t* out, size_t pitch, sr_stream stream) {
+    if (!out || row_begin < 0 || row_end > height || row_begin > row_end) return SR_E_INVALID;
+    int n = row_end - row_begin;
+    return launch(c, cam, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, pitch, nullptr, nullptr,
+                  stream);
+}
+
+int sr_blocks_row_count(int height, int block_rows, int block_first, int block_step) {
+    if (height <= 0 || block_rows <= 0 || block_first < 0 || block_step <= 0) return 0;
+    int rows = 0;
+    for (int b = block_first; b * block_rows < height; b += block_step) {
+        int r = height - b * block_rows;
+        rows += r < block_rows ? r : block_rows;
+    }
+    return rows;
+}
+
+int sr_render_blocks(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, int height, int block_rows,
+                     int block_first, int block_step, uint8_t* out, size_t pitch, sr_stream stream) {
+    if (!out || block_rows <= 0 || block_first < 0 || block_step <= 0) return SR_E_INVALID;
+    int nblocks = 0;
+    for (int b = block_first; b * block_rows < height; b += block_step) nblocks++;
+    return launch(c, cam, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
+                  block_step * block_rows, out, pitch, nullptr, nullptr, stream);
+}
+
+int sr_render_debug(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, int height, int row_begin,
+                    int row_end, float* dbg_rgba, uint8_t* out, int32_t* dbg_steps, sr_stream stream) {
+    if (row_begin < 0 || row_end > height || row_begin > row_end) return SR_E_INVALID;
+    if (!dbg_rgba && !out && !dbg_steps) return SR_E_INVALID;
+    int n = row_end - row_begin;
+    return launch(c, cam, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, (size_t)width * 4, dbg_rgba,
+                  dbg_steps, stream);
+}
+
+int sr_abi_struct_sizes(size_t* out, int n) {
+    const size_t sz[6] = {sizeof(sr_camera), sizeof(sr_params), sizeof(sr_scene),
+                          sizeof(sr_test_ray), sizeof(sr_material), sizeof(sr_light)};
+    if (!out || n < 0) return SR_E_INVALID;
+    for (int i = 0; i < n && i < 6; i++) out[i] = sz[i];
+    return SR_OK;
+}
+
+// Not in sr.h's public set: toggles segment culling (parity tests compare
+// culled and exhaustive renders bit for bit).
+int sr_debug_set_culling(sr_ctx* c, int enabled) {
+    if (!c) return SR_E_INVALID;
+    c->cull = enabled != 0;
+    return SR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""GPU renderer: a thin Python handle over the C-ABI (libsr.so).
+
+PyTorch only provides device memory and the HIP stream; every pixel is
+computed by the gfx950 kernel in libsr.so. There is no CPU fallback: without a
+HIP device `Renderer()` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class Renderer:
+    """One sr_ctx bound to one HIP device (the reference's single GL program)."""
+
+    def __init__(self, device: int = 0):
+        import torch
+
+        self.torch = torch
+        self.lib = abi.load()
+        self.device = int(device)
+        self.tdev = torch.device("cuda", self.device)
+        ctx = C.c_void_p()
+        abi.check(self.lib.sr_create(C.byref(ctx), self.device), "sr_create")
+        self.ctx = ctx
+        self._keep = []
+
+    # ---- uploads (src/main.cpp:205-274 equivalents) ----------------------------
+    def set_scene(self, scene: abi.Scene) -> None:
+        abi.check(self.lib.sr_set_scene(self.ctx, C.byref(scene)), "sr_set_scene")
+
+    def set_test_ray(self, test_ray: abi.TestRay) -> None:
+        abi.check(self.lib.sr_set_test_ray(self.ctx, C.byref(test_ray)), "sr_set_test_ray")
+
+    def set_background(self, img: np.ndarray) -> None:
+        img = np.ascontiguousarray(img, dtype=np.uint8)
+        h, w, ch = img.shape
+        abi.check(self.lib.sr_set_background(self.ctx, img.ctypes.data, w, h, ch), "sr_set_background")
+
+    def set_texture_array(self, arr: np.ndarray) -> None:
+        arr = np.ascontiguousarray(arr, dtype=np.uint8)
+        layers, h, w, ch = arr.shape
+        abi.check(self.lib.sr_set_texture_array(self.ctx, arr.ctypes.data, w, h, layers, ch), "sr_set_texture_array")
+
+    def set_culling(self, enabled: bool) -> None:
+        abi.check(self.lib.sr_debug_set_culling(self.ctx, 1 if enabled else 0), "sr_debug_set_culling")
+
+    # ---- rendering -------------------------------------------------------------
+    def _stream(self, stream):
+        if stream is None:
+            stream = self.torch.cuda.current_stream(self.tdev)
+        return C.c_void_p(stream.cuda_stream)
+
+    def render(self, cam: abi.Camera, params: abi.Params, width: int, height: int, row_begin: int = 0,
+               row_end: int | None = None, out=None, stream=None):
+        """RGBA8 rows [row_begin, row_end) (GL order, row 0 = bottom) into a
+        uint8 tensor [rows, width, 4] on this device. Asynchronous."""
+        row_end = height if row_end is None else row_end
+        rows = row_end - row_begin
+        if out is None:
+            out = self.torch.empty((max(rows, 0), width, 4), dtype=self.torch.uint8, device=self.tdev)
+        assert out.is_contiguous() and out.dtype == self.torch.uint8 and out.numel() >= rows * width * 4
+        abi.check(
+            self.lib.sr_render(self.ctx, C.byref(cam), C.byref(params), width, height, row_begin, row_end,
+                               C.c_void_p(out.data_ptr()), width * 4, self._stream(stream)),
+            "sr_render",
+        )
+        return out
+
+    def render_blocks(self, cam: abi.Camera, params: abi.Params, width: int, height: int, block_rows: int,
+                      block_first: int, block_step: int, out=None, stream=None):
+        """Block-cyclic row bands (multi-GPU tiling), packed densely."""
+        rows = self.lib.sr_blocks_row_count(height, block_rows, block_first, block_step)
+        nblocks = -(-rows // block_rows) if rows else 0
+        cap = nblocks * block_rows
+        if out is None:
+            out = self.torch.empty((cap, width, 4), dtype=self.torch.uint8, device=self.tdev)
+        assert out.is_contiguous() and out.numel() >= cap * width * 4
+        abi.check(
+            self.lib.sr_render_blocks(self.ctx, C.byref(cam), C.byref(params), width, height, block_rows,
+                                      block_first, block_step, C.c_void_p(out.data_ptr()), width * 4,
+                                      self._stream(stream)),
+            "sr_render_blocks",
+        )
+        return out, rows
+
+    def render_debug(self, cam: abi.Camera, params: abi.Params, width: int, height: int, row_begin: int = 0,
+                     row_end: int | None = None, stream=None):
+        """(float RGBA FragColor, RGBA8, executed steps) for rows [row_begin, row_end)."""
+        t = self.torch
+        row_end = height if row_end is None else row_end
+        rows = row_end - row_begin
+        f = t.empty((rows, width, 4), dtype=t.float32, device=self.tdev)
+        b = t.empty((rows, width, 4), dtype=t.uint8, device=self.tdev)
+        s = t.empty((rows, width), dtype=t.int32, device=self.tdev)
+        abi.check(
+            self.lib.sr_render_debug(self.ctx, C.byref(cam), C.byref(params), width, height, row_begin, row_end,
+                                     C.c_void_p(f.data_ptr()), C.c_void_p(b.data_ptr()), C.c_void_p(s.data_ptr()),
+                                     self._stream(stream)),
+            "sr_render_debug",
+        )
+        return f, b, s
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.sr_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

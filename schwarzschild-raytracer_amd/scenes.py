@@ -1,0 +1,193 @@
+"""Scene, camera and texture builders shared by tests, golden generation,
+smoke and bench.
+
+Textures are integer-procedural (bit-reproducible anywhere) stand-ins with the
+reference's shapes: the 2k skybox is 2048x1024 RGB (assets/textures/
+background/2k.jpg), the texture array holds uv_checker (600x600 RGB) and
+cubemap (1601x1201 RGBA), padded as loadTextureArray does
+(image_utils.cpp:42-117). The reference's JPEGs are not read at run time: the
+GPU box has no /root/reference.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+# ---- textures ----------------------------------------------------------------
+def skybox(width: int = 2048, height: int = 1024) -> np.ndarray:
+    """RGB8 equirectangular stand-in, rows bottom-up (already 'flipped')."""
+    x = np.arange(width, dtype=np.int64)[None, :]
+    y = np.arange(height, dtype=np.int64)[:, None]
+    r = (x * 255) // max(width - 1, 1) + 0 * y
+    g = (y * 255) // max(height - 1, 1) + 0 * x
+    cell = max(width // 64, 1)
+    b = np.where(((x // cell) + (y // cell)) % 2 == 0, 224, 48) + 0 * x + 0 * y
+    img = np.stack([r, g, b], axis=-1).astype(np.uint8)
+    return np.ascontiguousarray(img)
+
+
+def uv_checker(size: int = 600) -> np.ndarray:
+    """RGB8 stand-in for assets/textures/uv_checker.jpg (600x600)."""
+    x = np.arange(size, dtype=np.int64)[None, :]
+    y = np.arange(size, dtype=np.int64)[:, None]
+    cell = max(size // 10, 1)
+    r = np.where(((x // cell) + (y // cell)) % 2 == 0, 230, 30) + 0 * x + 0 * y
+    g = (x * 255) // max(size - 1, 1) + 0 * y
+    b = (y * 255) // max(size - 1, 1) + 0 * x
+    return np.ascontiguousarray(np.stack([r, g, b], axis=-1).astype(np.uint8))
+
+
+def cubemap(width: int = 1601, height: int = 1201) -> np.ndarray:
+    """RGBA8 stand-in for assets/textures/cubemap.png: a 4x3 cube-cross atlas,
+    opaque inside the six face cells and transparent outside (the box's uv
+    layout, frag:667-692)."""
+    x = np.arange(width, dtype=np.int64)[None, :]
+    y = np.arange(height, dtype=np.int64)[:, None]
+    cx = np.minimum((x * 4) // width, 3) + 0 * y
+    cy = np.minimum((y * 3) // height, 2) + 0 * x
+    faces = {(1, 0), (1, 1), (1, 2), (0, 1), (2, 1), (3, 1)}
+    inside = np.zeros((height, width), dtype=bool)
+    for fx, fy in faces:
+        inside |= (cx == fx) & (cy == fy)
+    r = (40 + 50 * cx) % 256
+    g = (40 + 70 * cy) % 256
+    b = (((x // 25) + (y // 25)) % 2) * 180 + 40
+    a = np.where(inside, 255, 0)
+    return np.ascontiguousarray(np.stack([r, g, b, a], axis=-1).astype(np.uint8))
+
+
+def pad_texture_array(images: list[np.ndarray]) -> tuple[np.ndarray, list[tuple[int, int]], tuple[int, int]]:
+    """image_utils.cpp:42-117: pad every layer to the max size/channels;
+    RGB sources get alpha 255 inside the image and 0 in the padding."""
+    max_w = max(im.shape[1] for im in images)
+    max_h = max(im.shape[0] for im in images)
+    max_c = max(im.shape[2] for im in images)
+    out_c = 4 if max_c == 4 else 3
+    arr = np.zeros((len(images), max_h, max_w, out_c), dtype=np.uint8)
+    sizes = []
+    for i, im in enumerate(images):
+        h, w, c = im.shape
+        arr[i, :h, :w, :c] = im[:, :, :out_c]
+        if out_c == 4 and c < 4:
+            arr[i, :h, :w, 3] = 255
+        sizes.append((w, h))
+    return np.ascontiguousarray(arr), sizes, (max_w, max_h)
+
+
+def default_texture_array():
+    """The app's texture array (src/main.cpp:210-218) with stand-in pixels."""
+    return pad_texture_array([uv_checker(600), cubemap(1601, 1201)])
+
+
+# ---- scenes --------------------------------------------------------------------
+def scene_default(textured: bool = True) -> abi.Scene:
+    """src/main.cpp:222-268 packed by the library's ObjectLoader mirror."""
+    s = abi.default_scene()
+    if not textured:
+        for m in range(abi.MAX_MATERIALS):
+            s.materials[m].texture_index = -1
+    return s
+
+
+def scene_black_hole_only() -> abi.Scene:
+    s = abi.Scene()
+    abi.load().sr_scene_clear(C.byref(s))
+    return s
+
+
+def set_scene_texture_sizes(s: abi.Scene, sizes, max_size) -> None:
+    for i, (w, h) in enumerate(sizes):
+        s.texture_sizes[i][0] = float(w)
+        s.texture_sizes[i][1] = float(h)
+    s.max_texture_size[0] = float(max_size[0])
+    s.max_texture_size[1] = float(max_size[1])
+
+
+# ---- cameras -------------------------------------------------------------------
+def _f32(x) -> np.float32:
+    return np.float32(x)
+
+
+def _normalize(v: np.ndarray) -> np.ndarray:
+    v = v.astype(np.float32)
+    d = np.float32(np.float32(v[0] * v[0]) + np.float32(v[1] * v[1])) + np.float32(v[2] * v[2])
+    k = np.float32(np.float32(1.0) / np.float32(np.sqrt(d)))
+    return (v * k).astype(np.float32)
+
+
+def _cross(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    return np.array(
+        [
+            np.float32(a[1] * b[2]) - np.float32(b[1] * a[2]),
+            np.float32(a[2] * b[0]) - np.float32(b[2] * a[0]),
+            np.float32(a[0] * b[1]) - np.float32(b[0] * a[1]),
+        ],
+        dtype=np.float32,
+    )
+
+
+def camera_look(pos, forward, right=None, fov: float = 90.0) -> abi.Camera:
+    """Camera(pos, forward, right) (camera.cpp:7-11); right defaults to
+    normalize(cross(forward, up)) as Camera::lookAt (camera.cpp:35-39)."""
+    pos = np.asarray(pos, dtype=np.float32)
+    f = _normalize(np.asarray(forward, dtype=np.float32))
+    if right is None:
+        right = _cross(f, np.array([0, 1, 0], dtype=np.float32))
+        if float(np.dot(right, right)) < 1e-12:
+            right = np.array([1, 0, 0], dtype=np.float32)
+    r_raw = np.asarray(right, dtype=np.float32)
+    r = _normalize(r_raw)
+    u = _normalize(_cross(r_raw, f))
+    cam = abi.Camera()
+    for i in range(3):
+        cam.transform.pos[i] = float(pos[i])
+        cam.transform.axes[i] = float(r[i])
+        cam.transform.axes[3 + i] = float(u[i])
+        cam.transform.axes[6 + i] = float(f[i])
+    cam.fov = float(fov)
+    return cam
+
+
+def random_camera(seed: int) -> abi.Camera:
+    """SURVEY §8d parity sweep: r ~ U[3, 50], direction uniform on S^2,
+    fov in {60, 90}; the camera looks at the hole with a random offset."""
+    rng = np.random.default_rng(seed)
+    r = rng.uniform(3.0, 50.0)
+    v = rng.normal(size=3)
+    v /= np.linalg.norm(v)
+    pos = (v * r).astype(np.float32)
+    target = rng.normal(size=3) * 0.35 * r
+    fwd = (target - pos).astype(np.float32)
+    fov = 60.0 if rng.integers(0, 2) == 0 else 90.0
+    return camera_look(pos, fwd, fov=fov)
+
+
+def camera_to_dict(cam: abi.Camera) -> dict:
+    return {"pos": list(cam.transform.pos), "axes": list(cam.transform.axes), "fov": cam.fov}
+
+
+def camera_from_arrays(pos, axes, fov) -> abi.Camera:
+    cam = abi.Camera()
+    for i in range(3):
+        cam.transform.pos[i] = float(pos[i])
+    for i in range(9):
+        cam.transform.axes[i] = float(axes[i])
+    cam.fov = float(fov)
+    return cam
+
+
+def struct_bytes(s) -> np.ndarray:
+    return np.frombuffer(bytes(memoryview(s)), dtype=np.uint8).copy()
+
+
+def struct_from_bytes(cls, data: np.ndarray):
+    obj = cls()
+    b = bytes(np.asarray(data, dtype=np.uint8))
+    if len(b) != C.sizeof(cls):
+        raise ValueError(f"{cls.__name__}: {len(b)} bytes, expected {C.sizeof(cls)}")
+    C.memmove(C.addressof(obj), b, len(b))
+    return obj

@@ -1,0 +1,210 @@
+"""HIP kernel (libsr.so, via the C-ABI) vs the CPU oracle.
+
+Contract: both sides evaluate the reference shader's float32
+expressions in the same order with the same rounding, so outputs are expected
+to be bit-identical: float FragColor, RGBA8 pixel and executed step count.
+The only allowed source of difference is the binary64 transcendental
+libraries (glibc on the host vs ocml on the device), which round to the same
+binary32 except when a result falls within one binary64 ulp of a binary32
+rounding boundary; the budget for that is MAX_MISMATCH_FRAC of pixels.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_case
+
+pytestmark = pytest.mark.gpu
+
+MAX_MISMATCH_FRAC = 1e-4  # tolerance: <= 0.01% of pixels may differ in any byte
+
+
+@pytest.fixture(scope="module")
+def gpu(pkg, textures):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    bg, arr = textures
+    r = pkg.Renderer(0)
+    r.set_background(bg)
+    r.set_texture_array(arr)
+    yield r
+    r.close()
+
+
+def gpu_debug(gpu, scene, cam, params, w, h, test_ray=None, row_begin=0, row_end=None):
+    import torch
+
+    gpu.set_scene(scene)
+    gpu.set_test_ray(test_ray if test_ray is not None else gpu_default_test_ray())
+    f, b, s = gpu.render_debug(cam, params, w, h, row_begin, row_end)
+    torch.cuda.synchronize()
+    return b.cpu().numpy(), f.cpu().numpy(), s.cpu().numpy()
+
+
+def gpu_default_test_ray():
+    import srpkg
+
+    return srpkg.load_package().abi.default_test_ray()
+
+
+def compare(gpu_out, ora_out, label):
+    b, f, s = gpu_out
+    rb, rf, rs = ora_out
+    px_diff = (b != rb).any(-1)
+    n = px_diff.size
+    frac = px_diff.mean()
+    steps_frac = (s != rs).mean()
+    fbits = (f.view(np.uint32) != rf.view(np.uint32)).any(-1) & ~(np.isnan(f).any(-1) & np.isnan(rf).any(-1))
+    msg = (f"{label}: rgba8 differ {px_diff.sum()}/{n}, float-bits differ {fbits.sum()}, "
+           f"steps differ {(s != rs).sum()}, max byte diff {np.abs(b.astype(int) - rb.astype(int)).max()}")
+    assert frac <= MAX_MISMATCH_FRAC, msg
+    assert steps_frac <= MAX_MISMATCH_FRAC, msg
+    return msg
+
+
+@pytest.fixture(scope="module")
+def oracle_tex(oracle, textures):
+    bg, arr = textures
+    return oracle.TextureSet(bg, arr)
+
+
+def test_golden_cases_bit_exact(pkg, gpu, oracle, oracle_tex, golden, golden_cases):
+    for name in golden_cases:
+        scene, cam, params, tr, w, h = load_case(pkg, golden, name)
+        g = gpu_debug(gpu, scene, cam, params, w, h, tr)
+        o = oracle.render(scene, cam, params, w, h, oracle_tex, tr)
+        print(compare(g, o, name))
+
+
+@pytest.mark.parametrize("seed", range(1, 17))
+def test_random_cameras(pkg, gpu, oracle, oracle_tex, seed):
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=bool(seed % 2))
+    cam = sc.random_camera(100 + seed)
+    params = abi.default_params(max_steps=400, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, cam, params, 80, 60)
+    o = oracle.render(scene, cam, params, 80, 60, oracle_tex)
+    compare(g, o, f"seed {seed}")
+
+
+@pytest.mark.parametrize("mode,cp", [(0, 0.5), (1, 0.5), (2, 0.37), (3, 0.61)])
+@pytest.mark.parametrize("filter_mode", [0, 1])
+def test_modes_and_filters(pkg, gpu, oracle, oracle_tex, mode, cp, filter_mode):
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=600, percent_black=-1.0, raytrace_type=mode, curved_percentage=cp,
+                                filter_mode=filter_mode, crosshair=1)
+    g = gpu_debug(gpu, scene, cam, params, 96, 54)
+    o = oracle.render(scene, cam, params, 96, 54, oracle_tex)
+    compare(g, o, f"mode {mode} filter {filter_mode}")
+
+
+def test_noise_mask(pkg, gpu, oracle, oracle_tex):
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=500, percent_black=0.75)
+    g = gpu_debug(gpu, scene, cam, params, 128, 72)
+    o = oracle.render(scene, cam, params, 128, 72, oracle_tex)
+    compare(g, o, "noise mask")
+    black = (g[0][..., :3] == 0).all(-1).mean()
+    assert 0.6 < black < 0.95
+
+
+def test_test_ray_overlay(pkg, gpu, oracle, oracle_tex):
+    """Press-R overlay (src/main.cpp:375-391, frag:760-803) with a long polyline."""
+    sc, abi = pkg.scenes, pkg.abi
+    cam0 = sc.camera_look((3.0, 2.0, 14.0), (-0.2, -0.1, -1.0))
+    fwd = list(cam0.transform.axes[6:9])
+    pts = abi.test_ray_points(list(cam0.transform.pos), fwd, 200, 2)
+    tr = abi.default_test_ray()
+    tr.visible = 1
+    tr.num_curved_points = len(pts)
+    for i, p in enumerate(pts):
+        tr.curved_points[i][0], tr.curved_points[i][1], tr.curved_points[i][2] = p
+    for k in range(3):
+        tr.flat_origin[k] = cam0.transform.pos[k] + fwd[k]
+        tr.flat_dir[k] = fwd[k]
+    view = sc.camera_look((8.0, 6.0, 20.0), (-8.0, -6.0, -20.0))
+    scene = sc.scene_default(textured=False)
+    params = abi.default_params(max_steps=200, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, view, params, 64, 36, tr)
+    o = oracle.render(scene, view, params, 64, 36, oracle_tex, tr)
+    compare(g, o, "test ray")
+    gpu.set_test_ray(abi.default_test_ray())
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_culling_is_exact(pkg, gpu, seed):
+    """Segment culling must not change a single bit (1080p-like aspect)."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera() if seed == 0 else sc.random_camera(200 + seed)
+    params = abi.default_params(max_steps=1000, percent_black=-1.0)
+    gpu.set_scene(scene)
+    outs = []
+    for cull in (True, False):
+        gpu.set_culling(cull)
+        f, b, s = gpu.render_debug(cam, params, 480, 270)
+        torch.cuda.synchronize()
+        outs.append((f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()))
+    gpu.set_culling(True)
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+
+
+def test_rows_and_blocks_assemble_full_frame(pkg, gpu):
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=500, percent_black=-1.0)
+    gpu.set_scene(scene)
+    W, H = 200, 113
+    full = gpu.render(cam, params, W, H).cpu().numpy()
+    part = gpu.render(cam, params, W, H, 37, 90).cpu().numpy()
+    assert np.array_equal(part, full[37:90])
+    for nranks in (2, 3, 8):
+        frame = np.zeros_like(full)
+        for rank in range(nranks):
+            out, rows = gpu.render_blocks(cam, params, W, H, 8, rank, nranks)
+            out = out.cpu().numpy()
+            k = 0
+            for b in range(rank, (H + 7) // 8, nranks):
+                n = min(8, H - b * 8)
+                frame[b * 8:b * 8 + n] = out[k:k + n]
+                k += n
+            assert k == rows
+        torch.cuda.synchronize()
+        assert np.array_equal(frame, full), nranks
+
+
+def test_headline_frame_sampled_rows(pkg, gpu, oracle, oracle_tex):
+    """1920x1080 / 2000 steps (the bench workload): 24 rows spread over the
+    frame bit-compared with the oracle, and run-to-run determinism."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+    W, H = 1920, 1080
+    gpu.set_scene(scene)
+    gpu.set_test_ray(abi.default_test_ray())
+    f, b, s = gpu.render_debug(cam, params, W, H)
+    b2 = gpu.render(cam, params, W, H)
+    torch.cuda.synchronize()
+    b, s, b2 = b.cpu().numpy(), s.cpu().numpy(), b2.cpu().numpy()
+    assert np.array_equal(b, b2)
+    rows = np.linspace(0, H - 1, 24).astype(int)
+    for y in rows:
+        rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
+        assert (rb[0] != b[y]).any(-1).mean() <= 1e-3, f"row {y}"
+        assert (rs[0] != s[y]).mean() <= 1e-3, f"row {y}"
+    # mean executed steps per pixel at N=2000 ~ 0.206 N
+    assert 380 < s.mean() < 440, s.mean()
