@@ -87,13 +87,9 @@ def main():
     r.set_texture_array(arr)
     r.set_culling(not args.no_cull)
 
-    nblocks = (H + BLOCK_ROWS - 1) // BLOCK_ROWS
-    my_blocks = len(range(rank, nblocks, world))
-    tile_rows = ((nblocks + world - 1) // world) * BLOCK_ROWS  # equal-size tiles for the gather
-    tile = torch.zeros((tile_rows, W, 4), dtype=torch.uint8, device=dev)
-    gathered = None
-    if distributed and rank == 0:
-        gathered = [torch.empty_like(tile) for _ in range(world)]
+    D = pkg.dist
+    tile = torch.zeros((D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
+    gather = D.FrameGather(tile, world, rank, H, BLOCK_ROWS)
     stream = torch.cuda.current_stream(dev)
 
     def render_tile():
@@ -101,13 +97,10 @@ def main():
 
     def step():
         render_tile()
-        if distributed:
-            dist.gather(tile, gathered if rank == 0 else None, dst=0)
+        return gather()  # the assembled frame on rank 0 (RCCL gather for N > 1)
 
     # executed steps of this rank's rows (untimed; the debug variant of the kernel)
-    rows_mine = []
-    for b in range(rank, nblocks, world):
-        rows_mine.extend(range(b * BLOCK_ROWS, min(H, (b + 1) * BLOCK_ROWS)))
+    rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
     _, _, steps_full = r.render_debug(cam, params, W, H)
     torch.cuda.synchronize(dev)
     sigma_steps_frame = int(steps_full.sum().item())

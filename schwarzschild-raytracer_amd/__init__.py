@@ -14,9 +14,9 @@ Layout:
 Import as a package via `load_package()` in bench.py / tests (the directory
 name is not a Python identifier).
 """
-from . import abi, scenes  # noqa: F401
+from . import abi, dist, scenes  # noqa: F401
 
-__all__ = ["abi", "scenes", "Renderer"]
+__all__ = ["abi", "dist", "scenes", "Renderer"]
 
 
 def __getattr__(name):

@@ -1,0 +1,96 @@
+"""The multi-GPU frame path (schwarzschild-raytracer_amd/dist.py) on CPU:
+world-size 2 and 3 process groups over gloo. Each rank renders its
+block-cyclic rows — here with the CPU oracle standing in for the GPU kernel,
+since this container has no GPU — packs them densely as sr_render_blocks
+does, and FrameGather brings the tiles to rank 0, which must reassemble the
+exact single-process frame."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+W, H, BR, STEPS = 48, 37, 8, 200
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import srpkg
+
+    pkg = srpkg.load_package()
+    oracle = srpkg.load_oracle()
+    D, sc, abi = pkg.dist, pkg.scenes, pkg.abi
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene = sc.scene_default(textured=False)
+        cam = abi.default_camera()
+        params = abi.default_params(max_steps=STEPS, percent_black=-1.0)
+        tile = torch.zeros((D.tile_rows(world, H, BR), W, 4), dtype=torch.uint8)
+        k = 0
+        for y in D.rows_of(rank, world, H, BR):
+            img, _, _ = oracle.render(scene, cam, params, W, H, None, None, y, y + 1, nthreads=1)
+            tile[k] = torch.from_numpy(img[0])
+            k += 1
+        frame = D.FrameGather(tile, world, rank, H, BR)()
+        if rank == 0:
+            q.put(frame.numpy().copy())
+        else:
+            assert frame is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_block_cyclic_gather_reassembles_frame(pkg, oracle, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frame = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    sc, abi = pkg.scenes, pkg.abi
+    ref, _, _ = oracle.render(sc.scene_default(textured=False), abi.default_camera(),
+                              abi.default_params(max_steps=STEPS, percent_black=-1.0), W, H)
+    assert np.array_equal(frame, ref)
+
+
+def test_partition_covers_every_row_once(pkg):
+    D = pkg.dist
+    for world in (1, 2, 4, 8):
+        for h in (1, 8, 37, 1080, 2160):
+            rows = sorted(r for k in range(world) for r in D.rows_of(k, world, h, 8))
+            assert rows == list(range(h))
+            assert max(len(D.rows_of(k, world, h, 8)) for k in range(world)) <= D.tile_rows(world, h, 8)
+
+
+def test_assemble_numpy_matches_loop(pkg):
+    D = pkg.dist
+    world, h = 3, 29
+    tr = D.tile_rows(world, h, 8)
+    stacked = np.zeros((world, tr, 2, 1), dtype=np.int32)
+    for r in range(world):
+        for k, y in enumerate(D.rows_of(r, world, h, 8)):
+            stacked[r, k] = y
+    frame = D.assemble(stacked, world, h, 8)
+    assert frame[:, 0, 0].tolist() == list(range(h))
