@@ -210,7 +210,7 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    p = Path(path) if path else Path(os.environ.get("SR_LIB", LIB_PATH))
     if not p.exists():
         raise FileNotFoundError(f"{p} not built; run __graft_entry__.build() or make -C schwarzschild-raytracer_amd")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)

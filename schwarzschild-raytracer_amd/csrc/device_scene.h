@@ -30,14 +30,33 @@
 #define SR_F_BOX_FACE0 16
 #define SR_F_FACE_STRIDE 14
 
+// How the step loop may skip an object's exact test (never changes a result):
+//   SR_KIND_EXACT  : always tested (planes, unbounded or non-orthonormal frames)
+//   SR_KIND_BUDGET : skipped while the path length since the last clearance
+//                    anchor is below the clearance budget (kernel: anchor_budget)
+//   SR_KIND_CHORD  : per-chord segment/bounding-sphere test (cylinders: the
+//                    margin depends on the chord direction)
+#define SR_KIND_EXACT 0
+#define SR_KIND_BUDGET 1
+#define SR_KIND_CHORD 2
+// Rounding margins, relative to S = |o|_1 + len + 1 of the chord:
+// a planar primitive's accepted hit point lies on the chord and passes a direct
+// distance test (error ~ eps * S); a quadratic's near-tangent root can wander
+// ~ sqrt(eps) * |o - c| (spheres, the black hole).
+#define SR_MU_PLANAR 1.0e-4f
+#define SR_MU_QUADRATIC 2.0e-3f
+
 typedef struct {
     int32_t type;
     int32_t index;
     int32_t material_index;
-    int32_t cull;    // 1: bounding sphere below is valid for segment culling
+    int32_t kind;    // SR_KIND_*
     float bc[3];     // bounding-sphere centre
-    float br;        // bounding-sphere radius (static margin included)
-    float f[SR_OBJ_FLOATS];
+    float br;        // bounding-sphere radius + static margin (per-chord test)
+    float rb;        // budget radius: br + SR_MU_QUADRATIC * (1 + |bc|_1 + br)
+    float mu;        // per-chord margin factor (SR_MU_*)
+    float mp;        // planar objects: plane-distance margin SR_MU_QUADRATIC * (1 + |pos|_1), else +inf
+    float f[SR_OBJ_FLOATS - 3];
 } sr_dev_obj;  // 512 B
 
 // One test-ray cylinder: pos[3] axes[9] height radius, padded to 16 floats.
@@ -50,7 +69,10 @@ typedef struct {
     int32_t tr_num_segments;  // num_test_ray_curved_points - 1 (>= 0)
     float tr_radius;
     float tr_extended_length;
-    float pad0[2];
+    int32_t num_budget;       // objects of SR_KIND_BUDGET
+    int32_t budget_idx[SR_MAX_OBJECTS];  // their indices in objs[]
+    int32_t num_step;         // objects of SR_KIND_EXACT / SR_KIND_CHORD (tested every step)
+    int32_t step_idx[SR_MAX_OBJECTS];
     float tr_curved_color[4];
     float tr_flat_color[4];
     float tr_flat[SR_SEG_FLOATS];  // flat test-ray cylinder

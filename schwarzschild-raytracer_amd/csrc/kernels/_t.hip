@@ -47,11 +47,11 @@ __device__ __forceinline__ float gmin(float x, float y) { return y < x ? y : x; 
 __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; }
 
 // binary64 function, rounded once to binary32
-__device__ __forceinline__ float t_sin(float x) { return (float)sin((double)x); }
-__device__ __forceinline__ float t_cos(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float t_asin(float x) { return (float)asin((double)x); }
-__device__ __forceinline__ float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __forceinline__ float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+__device__ __forceinline__ float t_sin(float x) { __builtin_amdgcn_sched_barrier(0); float r_ = (float)sin((double)x); __builtin_amdgcn_sched_barrier(0); return r_; }
+__device__ __forceinline__ float t_cos(float x) { __builtin_amdgcn_sched_barrier(0); float r_ = (float)cos((double)x); __builtin_amdgcn_sched_barrier(0); return r_; }
+__device__ __forceinline__ float t_asin(float x) { __builtin_amdgcn_sched_barrier(0); float r_ = (float)asin((double)x); __builtin_amdgcn_sched_barrier(0); return r_; }
+__device__ __forceinline__ float t_atan2(float y, float x) { __builtin_amdgcn_sched_barrier(0); float r_ = (float)atan2((double)y, (double)x); __builtin_amdgcn_sched_barrier(0); return r_; }
+__device__ __forceinline__ float t_pow(float x, float y) { __builtin_amdgcn_sched_barrier(0); float r_ = (float)pow((double)x, (double)y); __builtin_amdgcn_sched_barrier(0); return r_; }
 
 __device__ __forceinline__ f3 ld3(const float* p) { return F3(p[0], p[1], p[2]); }
 __device__ __forceinline__ m3 ldm(const float* a) {
@@ -322,11 +322,7 @@ __device__ __forceinline__ Hit closest_hit(const sr_dev_scene* __restrict__ sc, 
     // objects tested every step (planes: always; cylinders: unless the chord
     // misses their bounding sphere), then the budgeted ones when near
     const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + max_lambda + 1.0f;
-#ifdef SR_TIMING_NO_STEPOBJ  // timing experiments only
-    const int ns = 0;
-#else
     const int ns = sc->num_step;
-#endif
     for (int j = 0; j < ns; j++) {
         const int k = sc->step_idx[j];
         const sr_dev_obj& ob = sc->objs[k];
@@ -768,11 +764,7 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_geodesic_kernel(c
                 // wave-uniform: a wave runs the near path if any lane needs it, so
                 // every active lane tests and re-anchors together (keeps the
                 // lanes' anchors in step and the skipped steps coherent)
-#ifdef SR_TIMING_NO_NEAR  // timing experiments only
-                const bool near = false;
-#else
                 const bool near = __ballot(!(T * SR_BUDGET_SLACK < B)) != 0;
-#endif
                 hit = closest_hit(sc, segs, prev, rd, seg, cull, near);
                 if (cull && near) {  // re-anchor at the chord's end
                     B = anchor_budget(sc, ro);

@@ -77,14 +77,23 @@ bool orthonormal(V3 a, V3 b, V3 c) {
            std::fabs(dot(a, c)) < tol && std::fabs(dot(b, c)) < tol;
 }
 
-void set_bound(sr_dev_obj& o, V3 c, float R) {
+// Bounding sphere (c, R) of everything the object's exact test can accept.
+void set_bound(sr_dev_obj& o, V3 c, float R, int kind, float mu) {
     if (!std::isfinite(R) || !std::isfinite(c.x) || !std::isfinite(c.y) || !std::isfinite(c.z)) {
-        o.cull = 0;
+        o.kind = SR_KIND_EXACT;
         return;
     }
     st(o.bc, c);
-    o.br = R + 1e-4f * (1.f + l1norm(c) + R);
-    o.cull = 1;
+    o.br = R + mu * (1.f + l1norm(c) + R);
+    o.rb = R + SR_MU_QUADRATIC * (1.f + l1norm(c) + R);
+    o.mu = mu;
+    o.kind = kind;
+    // plane clearance (disk, hollow disk, rectangle): the plane through f[pos]
+    // with normal axes[1] must be a unit normal for |n.(A - pos)| to be a distance
+    V3 n = ld(o.f + SR_F_AXES + 3);
+    bool planar = o.type == SR_OBJECT_DISK || o.type == SR_OBJECT_HOLLOW_DISK || o.type == SR_OBJECT_RECTANGLE;
+    o.mp = planar && std::fabs(dot(n, n) - 1.f) < 1e-5f ? SR_MU_QUADRATIC * (1.f + l1norm(ld(o.f + SR_F_POS)))
+                                                         : INFINITY;
 }
 
 void put_transform(float* f, const sr_transform& t) {
@@ -124,19 +133,19 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         if (k < 0 || k >= SR_MAX_SPHERES) return SR_E_CAPACITY;
         put_transform(f, s.spheres[k].transform);
         f[SR_F_P0] = s.spheres[k].radius;
-        o.cull = 0;  // the sphere test is as cheap as the cull test
+        set_bound(o, ld(f), std::fabs(f[SR_F_P0]), SR_KIND_BUDGET, SR_MU_QUADRATIC);
         return SR_OK;
     }
     case SR_OBJECT_PLANE:
         if (k < 0 || k >= SR_MAX_PLANES) return SR_E_CAPACITY;
         put_plane(f, s.planes[k]);
-        o.cull = 0;  // unbounded
+        o.kind = SR_KIND_EXACT;  // unbounded
         return SR_OK;
     case SR_OBJECT_DISK: {
         if (k < 0 || k >= SR_MAX_DISKS) return SR_E_CAPACITY;
         put_plane(f, s.disks[k].plane);
         f[17] = s.disks[k].radius;
-        set_bound(o, ld(f), std::fabs(f[17]));
+        set_bound(o, ld(f), std::fabs(f[17]), SR_KIND_BUDGET, SR_MU_PLANAR);
         return SR_OK;
     }
     case SR_OBJECT_HOLLOW_DISK: {
@@ -144,7 +153,7 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         put_plane(f, s.hollow_disks[k].plane);
         f[17] = s.hollow_disks[k].inner_radius;
         f[18] = s.hollow_disks[k].outer_radius;
-        set_bound(o, ld(f), std::fabs(f[18]));
+        set_bound(o, ld(f), std::fabs(f[18]), SR_KIND_BUDGET, SR_MU_PLANAR);
         return SR_OK;
     }
     case SR_OBJECT_CYLINDER: {
@@ -156,7 +165,8 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         V3 a0 = ld(f + 3), a1 = ld(f + 6), a2 = ld(f + 9);
         if (orthonormal(a0, a1, a2) && h >= 0.f && r > 0.f) {
             double hh = 0.5 * h;
-            set_bound(o, add(ld(f), scl(a1, (float)hh)), (float)std::sqrt((double)r * r + hh * hh));
+            set_bound(o, add(ld(f), scl(a1, (float)hh)), (float)std::sqrt((double)r * r + hh * hh), SR_KIND_CHORD,
+                      SR_MU_PLANAR);
         }
         return SR_OK;
     }
@@ -169,7 +179,7 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         V3 a0 = ld(f + 3), a1 = ld(f + 6), a2 = ld(f + 9);
         if (orthonormal(a0, a1, a2) && w >= 0.f && h >= 0.f) {
             V3 c = add(ld(f), add(scl(a0, 0.5f * w), scl(a2, 0.5f * h)));
-            set_bound(o, c, (float)std::sqrt(0.25 * w * w + 0.25 * h * h));
+            set_bound(o, c, (float)std::sqrt(0.25 * w * w + 0.25 * h * h), SR_KIND_BUDGET, SR_MU_PLANAR);
         }
         return SR_OK;
     }
@@ -198,7 +208,7 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
             V3 c = add(p, mv(a0, a1, a2, v3(0.5f * b.width, 0.5f * b.height, 0.5f * b.depth)));
             double R = 0.5 * std::sqrt((double)b.width * b.width + (double)b.height * b.height +
                                        (double)b.depth * b.depth);
-            set_bound(o, c, (float)R);
+            set_bound(o, c, (float)R, SR_KIND_BUDGET, SR_MU_PLANAR);
         }
         return SR_OK;
     }
@@ -229,12 +239,14 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
     }
     // frag:860, 914-915, 925: the angle sequence depends only on the step index
     const float max_angle = 2.0f * (float)max_revs * kPi;
-    std::vector<float4> h((size_t)(max_steps > 0 ? max_steps : 1));
+    // entry i = {step_size, step_size / 6, cos phi, sin phi}; one padding entry
+    // so the kernel can prefetch i + 1 unconditionally
+    std::vector<float4> h((size_t)max_steps + 1, make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
     for (int i = 0; i < max_steps; i++) {
         float step = (max_angle - phi) / (float)(max_steps - i);
         phi += step;
-        h[i] = make_float4(step, phi, (float)std::cos((double)phi), (float)std::sin((double)phi));
+        h[i] = make_float4(step, step / 6.0f, (float)std::cos((double)phi), (float)std::sin((double)phi));
     }
     Table t;
     t.steps = max_steps;
@@ -418,9 +430,13 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
     d.num_objects = s->num_objects;
     d.num_lights = s->num_lights;
     std::memset(d.objs, 0, sizeof d.objs);
+    d.num_budget = 0;
+    d.num_step = 0;
     for (int i = 0; i < s->num_objects; i++) {
         int rc = pack_object(*s, i, d.objs[i]);
         if (rc != SR_OK) return rc;
+        if (d.objs[i].kind == SR_KIND_BUDGET) d.budget_idx[d.num_budget++] = i;
+        else d.step_idx[d.num_step++] = i;
     }
     std::memcpy(d.materials, s->materials, sizeof d.materials);
     std::memcpy(d.lights, s->lights, sizeof d.lights);

@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""A/B timing of libsr variants in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24). Each variant .so is loaded privately
+(RTLD_LOCAL) with its own context; the headline frame is rendered and the
+kernel timed with HIP events on the torch stream. Also checks every variant's
+frame is byte-identical to the first variant's.
+
+  python tools/ab_variants.py lib/variants/libsr_a.so lib/variants/libsr_b.so [--rounds 5 --reps 3]
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--camera", default="default")
+    ap.add_argument("--scene", choices=["tex", "untex", "bh"], default="tex")
+    args = ap.parse_args()
+    import torch
+
+    import srpkg
+
+    pkg = srpkg.load_package()
+    abi, sc = pkg.abi, pkg.scenes
+    scene = sc.scene_black_hole_only() if args.scene == "bh" else sc.scene_default(textured=args.scene == "tex")
+    cam = abi.default_camera() if args.camera == "default" else sc.random_camera(int(args.camera))
+    params = abi.default_params(max_steps=args.max_steps, percent_black=-1.0)
+    bg = np.ascontiguousarray(sc.skybox(2048, 1024))
+    arr, _, _ = sc.default_texture_array()
+    W, H = args.width, args.height
+    stream = torch.cuda.current_stream()
+    sp = C.c_void_p(stream.cuda_stream)
+    variants = []
+    for path in args.libs:
+        lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
+        for name, (res, argt) in {**abi.SIGNATURES, **abi.EXTRA_SIGNATURES}.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = res, argt
+        ctx = C.c_void_p()
+        abi.check(lib.sr_create(C.byref(ctx), 0), "sr_create")
+        abi.check(lib.sr_set_scene(ctx, C.byref(scene)), "scene")
+        abi.check(lib.sr_set_background(ctx, bg.ctypes.data, bg.shape[1], bg.shape[0], 3), "bg")
+        abi.check(lib.sr_set_texture_array(ctx, arr.ctypes.data, arr.shape[2], arr.shape[1], arr.shape[0], arr.shape[3]), "arr")
+        out = torch.empty((H, W, 4), dtype=torch.uint8, device="cuda")
+        variants.append((Path(path).name, lib, ctx, out))
+
+    def launch(v):
+        _, lib, ctx, out = v
+        abi.check(lib.sr_render(ctx, C.byref(cam), C.byref(params), W, H, 0, H, C.c_void_p(out.data_ptr()), W * 4, sp), "render")
+
+    for v in variants:
+        launch(v)
+    torch.cuda.synchronize()
+    nsteps = {}
+    for name, lib, ctx, out in variants:
+        st = torch.empty((H, W), dtype=torch.int32, device="cuda")
+        abi.check(lib.sr_render_debug(ctx, C.byref(cam), C.byref(params), W, H, 0, H, None, None,
+                                      C.c_void_p(st.data_ptr()), sp), "debug")
+        torch.cuda.synchronize()
+        nsteps[name] = int(st.sum().item())
+    ref = variants[0][3].cpu().numpy()
+    same = {v[0]: bool(np.array_equal(v[3].cpu().numpy(), ref)) for v in variants}
+    times = {v[0]: [] for v in variants}
+    for _ in range(args.rounds):
+        for v in variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(args.reps):
+                launch(v)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            times[v[0]].append(e0.elapsed_time(e1) / args.reps)
+    res = {k: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+               "mpix_s": W * H / (np.median(t) * 1e-3) / 1e6, "identical": same[k], "steps": nsteps[k],
+               "ps_per_step": np.median(t) * 1e9 / nsteps[k]} for k, t in times.items()}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
