@@ -33,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 # scene (integrator 71 + black hole 17 + six objects, all-miss) and per pixel.
 FLOP_PER_STEP = 360.0
 FLOP_PER_PIXEL = 150.0
+FLOP_PER_PIXEL_INTEGRATE = 100.0  # ray generation (P3, ~40) + orbital seed (P6, ~60); lighting is the shade kernel's
 # MI355X_MICROARCH.md: FP32 vector peak (packed FMA) and HBM3E peak.
 PEAK_FP32_TFLOPS = 157.3
 PEAK_FP32_UNPACKED_TFLOPS = 78.6
@@ -112,7 +113,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     # kernel-only timing with HIP events on the render stream (separate loop
-    # so the gather does not sit between the events)
+    # so the gather does not sit between the events); the library records
+    # per-kernel events (integrate / shade / resume) for the same frames
+    r.set_timing(args.steps)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
@@ -120,6 +123,9 @@ def main():
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    ktimes = r.kernel_times(args.steps)
+    r.set_timing(0)
+    integrate_ms, shade_ms, resume_ms = (float(x) for x in ktimes.mean(axis=0))
 
     if distributed:
         dist.barrier()
@@ -145,9 +151,11 @@ def main():
     mpix_s = W * H * args.steps / elapsed / 1e6
 
     if rank == 0:
-        # roofline of the dominant (only) kernel, on rank 0's launch
-        flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL
-        achieved_tflops = flop / (kernel_ms * 1e-3) / 1e12
+        # roofline of the dominant kernel (sr_integrate_kernel: ray generation,
+        # the step loop and every intersection test), on rank 0's launch
+        flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL_INTEGRATE
+        achieved_tflops = flop / (integrate_ms * 1e-3) / 1e12
+        frame_flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL
         hbm_bytes = len(rows_mine) * W * 4  # compulsory RGBA8 store; textures stay cache resident
         traffic = None
         tj = Path(args.traffic_json)
@@ -160,16 +168,25 @@ def main():
                 traffic = None
         roofline = {
             "bound": "valu",
+            "kernel": "sr_integrate_kernel",
             "achieved": round(achieved_tflops, 3),
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
             "traffic": traffic,
             "frac_unpacked_peak": round(achieved_tflops / PEAK_FP32_UNPACKED_TFLOPS, 4),
-            "kernel_ms": round(kernel_ms, 4),
+            "kernel_ms": round(integrate_ms, 4),
             "flop_per_launch": flop,
             "steps_per_launch": sigma_steps_mine,
             "mean_steps_per_pixel": round(sigma_steps_frame / (W * H), 2),
+            "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
+                            "resume": round(resume_ms, 4), "frame_events": round(kernel_ms, 4)},
+            "frame": {
+                "achieved": round(frame_flop / (kernel_ms * 1e-3) / 1e12, 3),
+                "unit": "TFLOP/s",
+                "flop_per_frame": frame_flop,
+                "frac": round(frame_flop / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
+            },
             "hbm": {
                 "achieved": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 3),
                 "peak": PEAK_HBM_GBS,

@@ -31,11 +31,11 @@
 #define SR_F_FACE_STRIDE 14
 
 // How the step loop may skip an object's exact test (never changes a result):
-//   SR_KIND_EXACT  : always tested (planes, unbounded or non-orthonormal frames)
-//   SR_KIND_BUDGET : skipped while the path length since the last clearance
-//                    anchor is below the clearance budget (kernel: anchor_budget)
-//   SR_KIND_CHORD  : per-chord segment/bounding-sphere test (cylinders: the
-//                    margin depends on the chord direction)
+//   SR_KIND_EXACT  : always tested (non-finite bounds, non-orthonormal frames)
+//   SR_KIND_BUDGET : held in a per-lane budget slot, skipped while the path
+//                    since the slot's anchor is below its clearance (kernel:
+//                    clearance / budget_step); planes by plane distance alone
+//   SR_KIND_CHORD  : per-chord segment/bounding-sphere test (budget slots full)
 #define SR_KIND_EXACT 0
 #define SR_KIND_BUDGET 1
 #define SR_KIND_CHORD 2
@@ -45,6 +45,17 @@
 // ~ sqrt(eps) * |o - c| (spheres, the black hole).
 #define SR_MU_PLANAR 1.0e-4f
 #define SR_MU_QUADRATIC 2.0e-3f
+// Cylinders: a near-tangent root of the lateral-surface quadratic can leave
+// the accepted point up to ~2 eps S^2 / (r |d_perp|^2) off the surface
+// (DESIGN.md §5); the margin below carries a ~30x safety factor.
+#define SR_CYL_QMARGIN 4.0e-6f
+// Budgeted cylinders: chords with |d_perp|^2 < SR_BUDGET_DPMIN are tested per
+// chord; the budget window is capped at SR_BUDGET_TMAX of path so the
+// quadratic margin can be bounded at the anchor.
+#define SR_BUDGET_DPMIN 0.02f
+#define SR_BUDGET_TMAX 8.0f
+// Objects held in the per-lane budget registers (index 0 is the black hole).
+#define SR_MAX_BUDGET 8
 
 typedef struct {
     int32_t type;
@@ -56,8 +67,17 @@ typedef struct {
     float rb;        // budget radius: br + SR_MU_QUADRATIC * (1 + |bc|_1 + br)
     float mu;        // per-chord margin factor (SR_MU_*)
     float mp;        // planar objects: plane-distance margin SR_MU_QUADRATIC * (1 + |pos|_1), else +inf
-    float f[SR_OBJ_FLOATS - 3];
+    float pl1;       // |pos|_1 (cylinder margins scale with |o - pos|)
+    float f[SR_OBJ_FLOATS - 4];
 } sr_dev_obj;  // 512 B
+
+// Per-pixel state planes passed between the integrate / shade / resume kernels
+// (geodesic.hip PS_*): status, step, steps, hit count, frag[4], ro, rd, nv, tv,
+// u, du, then SR_PS_HITS hit records {p[3], slot * 8 + face, chord dir[3], steps}.
+#define SR_PS_HITS 4
+#define SR_PS_FIELDS (24 + 8 * SR_PS_HITS)
+// Texture-array opacity bitmap radius (texels), see sr_api.cpp make_opacity_map
+#define SR_OPQ_RADIUS 2
 
 // One test-ray cylinder: pos[3] axes[9] height radius, padded to 16 floats.
 #define SR_SEG_FLOATS 16
@@ -69,8 +89,9 @@ typedef struct {
     int32_t tr_num_segments;  // num_test_ray_curved_points - 1 (>= 0)
     float tr_radius;
     float tr_extended_length;
-    int32_t num_budget;       // objects of SR_KIND_BUDGET
+    int32_t num_budget;       // objects of SR_KIND_BUDGET (<= SR_MAX_BUDGET)
     int32_t budget_idx[SR_MAX_OBJECTS];  // their indices in objs[]
+    int32_t budget_cyl_mask;  // bit j-1 set: budget slot j is a cylinder
     int32_t num_step;         // objects of SR_KIND_EXACT / SR_KIND_CHORD (tested every step)
     int32_t step_idx[SR_MAX_OBJECTS];
     float tr_curved_color[4];

@@ -76,6 +76,7 @@ struct Hit {
 struct Tex {
     const uint32_t* __restrict__ bg;
     const uint32_t* __restrict__ arr;
+    const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
 // ---- primitive tests: return the reference's is_hit and fill p ------------
@@ -185,7 +186,8 @@ __device__ __forceinline__ bool may_hit(const sr_dev_obj& ob, f3 o, f3 d, float 
         float dp = 1.0f - ca * ca;
         float r = ob.f[SR_F_P0 + 1];
         if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
-        R = R + 4.0e-6f * S * S * __builtin_amdgcn_rcpf(r * dp);
+        const float Sc = S + ob.pl1;  // the root error scales with |o - pos|
+        R = R + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp);
     }
     return !(d2 > R * R);
 }
@@ -259,69 +261,158 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
     }
 }
 
-// Clearance budget (not part of the reference; exact by margin). Every point
-// of the chords that follow an anchor point A on the ray's polyline lies
-// within T = (summed chord lengths since A) of A, so while
-//     T * (1 + 3 mu) < min_k(|A - c_k| - rb_k) - 1.8 mu |A|
-// no chord can come within rb_k (bounding radius + the per-chord rounding
-// margin mu * (|o|_1 + len + 1 + |c|_1 + R), |o|_1 <= 1.8 (|A| + T)) of any
-// budgeted object k or of the black hole: their exact tests cannot hit and
-// are skipped. Computed with hardware sqrt: its error is far below the margin.
-// Planar primitives (disk, hollow disk, rectangle) also accept only points
-// within ~eps*S of their plane (p = o + d*num/den leaves |n.(p - pos)| ~ eps*|num|),
-// so their clearance is the larger of the bounding-sphere and plane distances:
-// a thin accretion disk around the hole no longer exhausts the budget.
-#define SR_BUDGET_SLACK 1.006f
-__device__ __forceinline__ float anchor_budget(const sr_dev_scene* __restrict__ sc, f3 A) {
-    const float a = __builtin_amdgcn_sqrtf(dot(A, A));
-    float B = a - (1.0f + SR_MU_QUADRATIC * 3.0f);  // black hole: c = 0, R = 1
-    const int nb = sc->num_budget;
-    for (int j = 0; j < nb; j++) {
-        const sr_dev_obj& ob = sc->objs[sc->budget_idx[j]];
+// Clearance budgets (not part of the reference; exact by margin). Budget slot
+// 0 is the black hole, slot j >= 1 the object sc->objs[sc->budget_idx[j - 1]].
+// From an anchor point A on the ray's polyline, every point of the chords that
+// follow lies within T = (summed chord lengths since A) of A, so while
+//     T * SR_PATH_SLACK < clearance_j(A)
+// no chord can come within the per-chord acceptance region of slot j and its
+// exact test cannot hit: it is skipped. clearance_j(A) is
+//     max(|A - c| - rb, |n.(A - pos)| - mp)  (planar objects: the plane bound)
+//     - 1.8 mu_q |A|                         (chord origins |o|_1 <= 1.8 (|A| + T))
+// with rb = bounding radius + mu_q (1 + |c|_1 + R) and the path slack covering
+// the T-proportional part of the rounding margins. Cylinders also subtract
+// their quadratic margin SR_CYL_QMARGIN S^2 / (r SR_BUDGET_DPMIN) for the
+// largest S a chord of the window can have (windows are capped at
+// SR_BUDGET_TMAX); chords closer than SR_BUDGET_DPMIN to the cylinder axis
+// direction are tested per chord instead (budget_parallel). Computed with
+// hardware sqrt: its error is far below the margins.
+#define SR_PATH_SLACK 1.01f
+__device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
+    float c;
+    if (j == 0) {
+        c = a - (1.0f + SR_MU_QUADRATIC * 3.0f);  // black hole: centre 0, R = 1
+    } else {
+        const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
         f3 w = A - ld3(ob.bc);
-        float clear = __builtin_amdgcn_sqrtf(dot(w, w)) - ob.rb;
-        if (ob.type == SR_OBJECT_DISK || ob.type == SR_OBJECT_HOLLOW_DISK || ob.type == SR_OBJECT_RECTANGLE) {
+        c = __builtin_amdgcn_sqrtf(dot(w, w)) - ob.rb;
+        if (ob.type == SR_OBJECT_PLANE || ob.type == SR_OBJECT_DISK || ob.type == SR_OBJECT_HOLLOW_DISK ||
+            ob.type == SR_OBJECT_RECTANGLE) {
             f3 q = A - ld3(ob.f + SR_F_POS);
-            clear = fmaxf(clear, fabsf(dot(q, ld3(ob.f + SR_F_AXES + 3))) - ob.mp);
+            c = fmaxf(c, fabsf(dot(q, ld3(ob.f + SR_F_AXES + 3))) - ob.mp);
+        } else if (ob.type == SR_OBJECT_CYLINDER) {
+            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + ob.pl1 + (3.0f * SR_BUDGET_TMAX + 1.0f);
+            float qm = SR_CYL_QMARGIN * Sb * Sb / (ob.f[SR_F_P0 + 1] * SR_BUDGET_DPMIN);
+            c = fminf(c - qm, SR_BUDGET_TMAX);
         }
-        B = fminf(B, clear);
     }
-    return B - 1.8f * SR_MU_QUADRATIC * a;
+    return c - 1.8f * SR_MU_QUADRATIC * a;
 }
 
-// intersect(), frag:755-814: the closest hit along [o, o + max_lambda*d]
-// (max_lambda < 0: unbounded). `cull` enables skipping exact tests that
-// provably miss: budgeted objects and the black hole unless `near`, chord-
-// culled objects when the chord misses their bounding sphere.
-__device__ __forceinline__ Hit closest_hit(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs, f3 o, f3 d,
-                           float max_lambda, bool cull, bool near) {
-    Hit best = no_hit();
-    f3 p;
-    cull = cull && max_lambda >= 0.0f;
-    if (!cull || near)  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
-        consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, max_lambda, p), p, o, SLOT_BH, 0, KEY_BH);
+// A budgeted cylinder's window margin holds only for chords whose direction
+// keeps |d_perp|^2 >= SR_BUDGET_DPMIN; others are tested regardless.
+__device__ __forceinline__ bool budget_parallel(const sr_dev_scene* __restrict__ sc, int j, f3 d) {
+    if (j == 0 || !((sc->budget_cyl_mask >> (j - 1)) & 1)) return false;
+    const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
+    float ca = dot(d, ld3(ob.f + SR_F_AXES + 3));
+    return !(1.0f - ca * ca >= SR_BUDGET_DPMIN);
+}
 
-    if (sc->tr_visible) {  // frag:760-803
-        const float* t = sc->tr_flat;
-        m3 A = ldm(t + 3);
-        consider(best, cyl_test(o, d, ld3(t), A, t[12], t[13], max_lambda, p), p, o, SLOT_TR_FLAT, 0, KEY_TR_FLAT);
-        int ns = sc->tr_num_segments;
-        for (int s = 0; s < ns; s++) {
-            const float* g = segs + s * SR_SEG_FLOATS;
-            m3 B = ldm(g + 3);
-            consider(best, cyl_test(o, d, ld3(g), B, g[12], g[13], max_lambda, p), p, o, SLOT_TR_CURVED, 0,
-                     KEY_TR_CURVED0 + s);
+// NaN-propagating minimum: a NaN clearance must force the exact tests.
+__device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e : m; }
+
+// Per-lane budget state: E[j] = clearance_j(anchor_j) - slacked path from
+// anchor_j to the last budget event, T = slacked path since that event,
+// m = min_j E[j]. Slots re-anchor independently: only those whose budget is
+// spent are tested and re-anchored.
+struct Budget {
+    float E[SR_MAX_BUDGET + 1];
+    float T, m;
+};
+
+__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A) {
+    const float a = __builtin_amdgcn_sqrtf(dot(A, A));
+    const int nb = sc->num_budget;
+    bs.T = 0.0f;
+    bs.m = INFINITY;
+#pragma unroll
+    for (int j = 0; j <= SR_MAX_BUDGET; j++) {
+        if (j <= nb) {
+            bs.E[j] = clearance(sc, j, A, a);
+            bs.m = nmin(bs.m, bs.E[j]);
         }
     }
+}
 
-    if (!cull) {
-        const int n = sc->num_objects;
-        for (int k = 0; k < n; k++) test_object(best, sc->objs[k], k, o, d, max_lambda);
-        return best;
+// Intersect objects[] and the black hole in budget slots with the chord
+// [o, o + seg*d] (ending at `end`) where the budget requires it, and advance
+// the budgets. The branch structure is wave-uniform (ballots).
+__device__ __forceinline__ void budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, Hit& best, f3 o, f3 d,
+                                            float seg, float S, f3 end) {
+    bs.T += seg * SR_PATH_SLACK;
+    bool fire = !(bs.T < bs.m);
+    const int nb = sc->num_budget;
+    const int cm = sc->budget_cyl_mask;
+    if (cm) {
+#pragma unroll
+        for (int j = 1; j <= SR_MAX_BUDGET; j++) {
+            if (j <= nb) fire = fire || budget_parallel(sc, j, d);
+        }
     }
-    // objects tested every step (planes: always; cylinders: unless the chord
-    // misses their bounding sphere), then the budgeted ones when near
-    const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + max_lambda + 1.0f;
+    if (!__ballot(fire)) return;
+    const float a = __builtin_amdgcn_sqrtf(dot(end, end));
+    float m = INFINITY;
+#pragma unroll
+    for (int j = 0; j <= SR_MAX_BUDGET; j++) {
+        if (j > nb) continue;
+        if (__ballot(!(bs.T < bs.E[j]) || budget_parallel(sc, j, d))) {
+            f3 p;
+            if (j == 0) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
+                consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, seg, p), p, o, SLOT_BH, 0, KEY_BH);
+            } else {
+                const int k = sc->budget_idx[j - 1];
+                const sr_dev_obj& ob = sc->objs[k];
+                if (may_hit(ob, o, d, seg, S)) test_object(best, ob, k, o, d, seg);
+            }
+            bs.E[j] = clearance(sc, j, end, a);
+        } else {
+            bs.E[j] = bs.E[j] - bs.T;
+        }
+        m = nmin(m, bs.E[j]);
+    }
+    bs.T = 0.0f;
+    bs.m = m;
+}
+
+// The test rays (frag:760-803), visited right after the black hole.
+__device__ __forceinline__ void test_ray_hits(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                              Hit& best, f3 o, f3 d, float max_lambda) {
+    if (!sc->tr_visible) return;
+    f3 p;
+    const float* t = sc->tr_flat;
+    m3 A = ldm(t + 3);
+    consider(best, cyl_test(o, d, ld3(t), A, t[12], t[13], max_lambda, p), p, o, SLOT_TR_FLAT, 0, KEY_TR_FLAT);
+    int ns = sc->tr_num_segments;
+    for (int s = 0; s < ns; s++) {
+        const float* g = segs + s * SR_SEG_FLOATS;
+        m3 B = ldm(g + 3);
+        consider(best, cyl_test(o, d, ld3(g), B, g[12], g[13], max_lambda, p), p, o, SLOT_TR_CURVED, 0,
+                 KEY_TR_CURVED0 + s);
+    }
+}
+
+// intersect(), frag:755-814, exhaustively: the closest hit along
+// [o, o + max_lambda*d] (max_lambda < 0: unbounded).
+__device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                               f3 o, f3 d, float max_lambda) {
+    Hit best = no_hit();
+    f3 p;
+    consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, max_lambda, p), p, o, SLOT_BH, 0, KEY_BH);
+    test_ray_hits(sc, segs, best, o, d, max_lambda);
+    const int n = sc->num_objects;
+    for (int k = 0; k < n; k++) test_object(best, sc->objs[k], k, o, d, max_lambda);
+    return best;
+}
+
+// intersect() for one chord of the step loop with culling: the test rays, the
+// objects tested every step (chord-culled ones only when the chord reaches
+// their bounding sphere), then the budget slots. Same winner as
+// closest_hit_all (lexicographic keys, skipped tests provably miss).
+__device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                                 Budget& bs, f3 o, f3 d, float seg, f3 end) {
+    Hit best = no_hit();
+    test_ray_hits(sc, segs, best, o, d, seg);
+    const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;
 #ifdef SR_TIMING_NO_STEPOBJ  // timing experiments only
     const int ns = 0;
 #else
@@ -330,18 +421,10 @@ __device__ __forceinline__ Hit closest_hit(const sr_dev_scene* __restrict__ sc, 
     for (int j = 0; j < ns; j++) {
         const int k = sc->step_idx[j];
         const sr_dev_obj& ob = sc->objs[k];
-        if (ob.kind == SR_KIND_CHORD && !may_hit(ob, o, d, max_lambda, S)) continue;
-        test_object(best, ob, k, o, d, max_lambda);
+        if (ob.kind == SR_KIND_CHORD && !may_hit(ob, o, d, seg, S)) continue;
+        test_object(best, ob, k, o, d, seg);
     }
-    if (near) {
-        const int nb = sc->num_budget;
-        for (int j = 0; j < nb; j++) {
-            const int k = sc->budget_idx[j];
-            const sr_dev_obj& ob = sc->objs[k];
-            if (!may_hit(ob, o, d, max_lambda, S)) continue;
-            test_object(best, ob, k, o, d, max_lambda);
-        }
-    }
+    budget_step(sc, bs, best, o, d, seg, S, end);
     return best;
 }
 
@@ -419,8 +502,18 @@ struct Surface {
     float theta;  // sphere
 };
 
-__device__ __forceinline__ float phi_of(f3 local) {
-    float phi = t_atan2(local.x, local.z);
+// APPROX: the binary32 library atan2 (a few ulp from the binary64-rounded
+// value) for the step loop's opacity classification; `ok` turns false near the
+// 0 / 2pi seam, where the two can land on opposite sides.
+template <bool APPROX>
+__device__ __forceinline__ float phi_of(f3 local, bool& ok) {
+    float phi;
+    if (APPROX) {
+        phi = atan2f(local.x, local.z);
+        ok = ok && fabsf(phi) > 1.0e-3f;
+    } else {
+        phi = t_atan2(local.x, local.z);
+    }
     if (phi < 0.0f) phi += 2.0f * SR_PI;
     return phi;
 }
@@ -441,7 +534,11 @@ __device__ __forceinline__ m3 box_face(const float* f, int face) {
     return F;
 }
 
-__device__ Surface surface_of(const sr_dev_obj& ob, const Hit& h) {
+// tangent_space + tangent_coordinates of a hit (frag:208-333). APPROX (the step
+// loop's opacity test): binary32 atan2 / asin, `ok` false where that may
+// move the uv across a seam; every other operation is the exact one.
+template <bool APPROX>
+__device__ __forceinline__ Surface surface_of_t(const sr_dev_obj& ob, const Hit& h, bool& ok) {
     const float* f = ob.f;
     f3 pos = ld3(f + SR_F_POS);
     m3 A = ldm(f + SR_F_AXES);
@@ -453,15 +550,15 @@ __device__ Surface surface_of(const sr_dev_obj& ob, const Hit& h) {
     case SR_OBJECT_SPHERE: {  // frag:209-232
         s.n = nrm(disp);
         f3 local = mtv(A, disp);
-        s.phi = phi_of(local);
-        s.theta = t_asin(local.y / f[SR_F_P0]);
+        s.phi = phi_of<APPROX>(local, ok);
+        s.theta = APPROX ? asinf(local.y / f[SR_F_P0]) : t_asin(local.y / f[SR_F_P0]);
         s.uv = F2(s.phi / (2.0f * SR_PI), s.theta / SR_PI + 0.5f);
         return s;
     }
     case SR_OBJECT_DISK:
     case SR_OBJECT_HOLLOW_DISK: {  // frag:249-295
         f3 local = mtv(A, disp);
-        s.phi = phi_of(local);
+        s.phi = phi_of<APPROX>(local, ok);
         if (ob.type == SR_OBJECT_DISK) s.uv = F2(len(local) / f[17], s.phi / (2.0f * SR_PI));
         else s.uv = F2((len(local) - f[17]) / (f[18] - f[17]), s.phi / (2.0f * SR_PI));
         s.n = A.c1;
@@ -470,7 +567,7 @@ __device__ Surface surface_of(const sr_dev_obj& ob, const Hit& h) {
     case SR_OBJECT_CYLINDER: {  // frag:297-318
         s.n = nrm(disp);
         f3 local = mtv(A, disp);
-        s.phi = phi_of(local);
+        s.phi = phi_of<APPROX>(local, ok);
         s.uv = F2(s.phi / (2.0f * SR_PI), local.y / f[SR_F_P0]);
         return s;
     }
@@ -500,6 +597,11 @@ __device__ Surface surface_of(const sr_dev_obj& ob, const Hit& h) {
         s.n = A.c1;
         return s;
     }
+}
+
+__device__ Surface surface_of(const sr_dev_obj& ob, const Hit& h) {
+    bool ok = true;
+    return surface_of_t<false>(ob, h, ok);
 }
 
 // The full tangent_space matrix (normal-map path only); n is the (possibly
@@ -630,10 +732,88 @@ __device__ __forceinline__ f4 shade(const sr_dev_scene* __restrict__ sc, const s
     return c;
 }
 
+// Opacity of calculate_lighting's result for a chord hit, decided in the step
+// loop without lighting (exact where it claims):
+//   OP_OPAQUE: alpha == 1 exactly, the ray ends here (frag:932)
+//   OP_ZERO  : vec4(0) (a single-sided surface seen from behind, frag:370-374):
+//              adding it leaves frag unchanged (frag starts at +0 or 0.5 and
+//              is never -0), the ray goes on
+//   OP_MAYBE : anything else; the hit is queued for shading and the ray goes on
+// Textured alpha: the bilinear footprint is located with binary32 uv (within
+// far less than a texel of the shaded one) and is opaque when the opacity
+// bitmap says every texel within SR_OPQ_RADIUS of it has alpha 255 (LERP
+// filtering of four 1.0 alphas is exactly 1.0).
+#define OP_OPAQUE 0
+#define OP_ZERO 1
+#define OP_MAYBE 2
+__device__ __forceinline__ int hit_opacity_uniform(const sr_dev_scene* __restrict__ sc, const sr_dev_frame& fr,
+                                                   const Tex& tx, int slot, int face, const Hit& hit, f3 view_dir,
+                                                   bool zero_only) {
+    if (slot == SLOT_BH) return OP_OPAQUE;
+    if (slot == SLOT_TR_CURVED) return sc->tr_curved_color[3] == 1.0f ? OP_OPAQUE : OP_MAYBE;
+    if (slot == SLOT_TR_FLAT) return sc->tr_flat_color[3] == 1.0f ? OP_OPAQUE : OP_MAYBE;
+    const sr_dev_obj& ob = sc->objs[slot];
+    int mi = ob.material_index;
+    if (mi < 0 || mi >= SR_MAX_MATERIALS) mi = 0;
+    const sr_material& m = sc->materials[mi];
+    if (!m.double_sided_normals) {  // surface_of's normal, then flip_normals (shade_hit)
+        const float* f = ob.f;
+        f3 n;
+        if (ob.type == SR_OBJECT_SPHERE || ob.type == SR_OBJECT_CYLINDER)
+            n = nrm(hit.p - ld3(f + SR_F_POS));
+        else if (ob.type == SR_OBJECT_BOX)
+            n = ld3(f + SR_F_BOX_FACE0 + SR_F_FACE_STRIDE * face + 6);
+        else
+            n = ld3(f + SR_F_AXES + 3);
+        if (m.flip_normals) n = n * -1.0f;
+        if (dot(n, view_dir) < 0.0f) return OP_ZERO;
+    }
+    if (zero_only) return OP_MAYBE;
+    if (m.texture_index < 0) return m.color[3] == 1.0f ? OP_OPAQUE : OP_MAYBE;
+    if (ob.type == SR_OBJECT_PLANE || fr.filter_mode != SR_FILTER_LERP || !tx.opq || !tx.arr || fr.arr_w <= 0 ||
+        fr.arr_h <= 0 || fr.arr_layers <= 0)
+        return OP_MAYBE;
+    Hit hh = hit;
+    hh.face = face;
+    bool ok = true;
+    f2 uv = surface_of_t<true>(ob, hh, ok).uv;
+    if (!ok) return OP_MAYBE;
+    if (m.swap_uvs) uv = F2(uv.y, uv.x);
+    if (m.invert_uv_x) uv.x = 1.0f - uv.x;
+    if (m.invert_uv_y) uv.y = 1.0f - uv.y;
+    const int ti = m.texture_index < SR_MAX_TEXTURES ? m.texture_index : 0;
+    f2 r = F2((uv.x * sc->texture_sizes[ti][0]) / sc->max_texture_size[0],
+              (uv.y * sc->texture_sizes[ti][1]) / sc->max_texture_size[1]);
+    int layer = m.texture_index;
+    if (layer > fr.arr_layers - 1) layer = fr.arr_layers - 1;
+    const float s = r.x * (float)fr.arr_w - 0.5f;  // bilinear()
+    const float t = r.y * (float)fr.arr_h - 0.5f;
+    if (!(fabsf(s) < 4194304.0f) || !(fabsf(t) < 4194304.0f)) return OP_MAYBE;
+    const int x = wrap_rep(floorf(s), fr.arr_w), y = wrap_rep(floorf(t), fr.arr_h);
+    const size_t stride = ((size_t)fr.arr_w + 7) >> 3;
+    const uint8_t bits = tx.opq[((size_t)layer * (size_t)fr.arr_h + (size_t)y) * stride + (size_t)(x >> 3)];
+    return (bits >> (x & 7)) & 1 ? OP_OPAQUE : OP_MAYBE;
+}
+
+__device__ __forceinline__ int hit_opacity(const sr_dev_scene* __restrict__ sc, const sr_dev_frame& fr,
+                                           const Tex& tx, const Hit& hit, f3 view_dir, bool zero_only) {
+    const int key = hit.slot * 8 + hit.face;
+    int op;
+    for (;;) {  // waterfall: object data as wave-uniform loads
+        const int first = __builtin_amdgcn_readfirstlane(key);
+        if (key == first) {
+            op = hit_opacity_uniform(sc, fr, tx, __builtin_amdgcn_readfirstlane(hit.slot),
+                                     __builtin_amdgcn_readfirstlane(hit.face), hit, view_dir, zero_only);
+            break;
+        }
+    }
+    return op;
+}
+
 __device__ __forceinline__ f4 intersect_color(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                               const sr_dev_frame& fr, const Tex& tx, f3 o, f3 d,
-                                              float max_lambda, bool cull, bool near) {
-    Hit h = closest_hit(sc, segs, o, d, max_lambda, cull, near);
+                                              float max_lambda) {
+    Hit h = closest_hit_all(sc, segs, o, d, max_lambda);
     if (h.slot == SLOT_NONE) return F4(0.0f, 0.0f, 0.0f, 0.0f);
     return shade(sc, fr, tx, h, -d);
 }
@@ -644,185 +824,384 @@ __device__ __forceinline__ uint32_t unorm8(float x) {
     return (uint32_t)floorf(x * 255.0f + 0.5f);
 }
 
-}  // namespace
+// ---- pixel pipeline ---------------------------------------------------------
+// A frame is three launches on one stream:
+//   sr_integrate_kernel : camera ray + RK4 step loop (integration registers
+//                         only). Chord hits are classified by hit_opacity:
+//                         back faces are skipped, hits that may be translucent
+//                         are recorded and the ray goes on, the first opaque
+//                         hit (or the end of the ray) stops it
+//   sr_shade_kernel     : calculate_lighting of the recorded hits in order,
+//                         skybox / unbounded flat intersect, final pixels; a
+//                         pixel whose recorded hits were all translucent and
+//                         whose ray stopped early is queued for resumption
+//   sr_resume_kernel    : the queued pixels (dense worklist), integrated and
+//                         shaded in rounds to completion
+// Pixel state between launches lives in SoA planes ps[field * n + id], id = the
+// pixel's thread index in the launch grid (coalesced for every kernel).
+#define ST_DONE 0  // no ray (percent_black): frag = the crosshair colour
+#define ST_HIT 1   // stopped at an opaque-classified hit (the last recorded one)
+#define ST_MORE 2  // stopped with SR_PS_HITS translucent hits recorded
+#define ST_FLAT 3  // unbounded intersect(ray), then get_bg if alpha != 1 (frag:874-876, 895-897, 903-905)
+#define ST_BG 4    // get_bg(rd) (frag:921-922 break, 935)
 
-// Exit modes of the step loop
-#define MODE_DONE 1   // FragColor final
-#define MODE_FLAT 2   // unbounded intersect(ray), then get_bg if alpha != 1 (frag:874-876, 895-897, 903-905)
-#define MODE_BG 3     // get_bg(ray.dir) (frag:921-922 break, 935)
+enum {
+    PS_STATUS = 0, PS_I = 1, PS_STEPS = 2, PS_NHITS = 3, PS_FRAG = 4, PS_RO = 8, PS_RD = 11, PS_NV = 14, PS_TV = 17,
+    PS_U = 20, PS_DU = 21, PS_HIT0 = 24, PS_HIT_STRIDE = 8  // hit j: p[3], slot * 8 + face, chord dir[3], steps
+};
+static_assert(PS_HIT0 + PS_HIT_STRIDE * SR_PS_HITS == SR_PS_FIELDS, "pixel-state layout");
 
-#ifndef SR_MIN_WAVES_PER_EU
-#define SR_MIN_WAVES_PER_EU 1
-#endif
+struct Ray {
+    f3 ro, rd, nv, tv;
+    float u, du;
+    int i, steps;
+};
 
-template <bool DEBUG>
-__global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_geodesic_kernel(const sr_dev_scene* __restrict__ sc,
-                                                          const float4* __restrict__ tbl,
-                                                          const float* __restrict__ segs,
-                                                          const uint32_t* __restrict__ bg,
-                                                          const uint32_t* __restrict__ arr,
-                                                          sr_dev_frame fr, uint8_t* __restrict__ out,
-                                                          size_t pitch, float* __restrict__ dbg_rgba,
-                                                          int32_t* __restrict__ dbg_steps) {
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int px = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int k = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    if (px >= fr.width || k >= fr.nrows) return;
-    const int py = fr.row_base + (k / fr.block_rows) * fr.block_stride + (k % fr.block_rows);
-    if (py >= fr.height) return;
+struct Pix {
+    int px, k, py;
+};
 
-    Tex tx;
-    tx.bg = bg;
-    tx.arr = arr;
-    const bool cull = fr.cull != 0;
+// 16x16 workgroup tile of four 8x8 wave tiles; false for threads off the frame
+__device__ __forceinline__ bool pixel_of(const sr_dev_frame& fr, int block, int t, Pix& q) {
+    const int gx = (fr.width + 15) >> 4;
+    const int bx = block % gx, by = block / gx;
+    const int lane = t & 63, wave = t >> 6;
+    q.px = bx * 16 + (wave & 1) * 8 + (lane & 7);
+    q.k = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+    if (q.px >= fr.width || q.k >= fr.nrows) return false;
+    q.py = fr.row_base + (q.k / fr.block_rows) * fr.block_stride + (q.k % fr.block_rows);
+    return q.py < fr.height;
+}
 
-    // full_screen_quad.vert:7-10: uv = NDC of the pixel centre
-    f2 uv = F2((float)(2 * px + 1) / (float)fr.width - 1.0f, (float)(2 * py + 1) / (float)fr.height - 1.0f);
+struct PS {
+    float* __restrict__ p;
+    size_t n;
+    __device__ __forceinline__ float& at(int f, size_t id) const { return p[(size_t)f * n + id]; }
+    __device__ __forceinline__ void put3(int f, size_t id, f3 v) const {
+        at(f, id) = v.x;
+        at(f + 1, id) = v.y;
+        at(f + 2, id) = v.z;
+    }
+    __device__ __forceinline__ f3 get3(int f, size_t id) const { return F3(at(f, id), at(f + 1, id), at(f + 2, id)); }
+    __device__ __forceinline__ void puti(int f, size_t id, int v) const { at(f, id) = __int_as_float(v); }
+    __device__ __forceinline__ int geti(int f, size_t id) const { return __float_as_int(at(f, id)); }
+    __device__ __forceinline__ void put4(int f, size_t id, f4 v) const {
+        at(f, id) = v.x;
+        at(f + 1, id) = v.y;
+        at(f + 2, id) = v.z;
+        at(f + 3, id) = v.w;
+    }
+    __device__ __forceinline__ f4 get4(int f, size_t id) const {
+        return F4(at(f, id), at(f + 1, id), at(f + 2, id), at(f + 3, id));
+    }
+};
+
+// frag:845-857: the crosshair's initial FragColor
+__device__ __forceinline__ f4 crosshair_frag(const sr_dev_frame& fr, const Pix& q) {
     f4 frag = F4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (fr.crosshair) {  // frag:845-857
+    if (fr.crosshair) {
+        f2 uv = F2((float)(2 * q.px + 1) / (float)fr.width - 1.0f, (float)(2 * q.py + 1) / (float)fr.height - 1.0f);
         float hx = fabsf(uv.x * fr.res_x / 2.0f), hy = fabsf(uv.y * fr.res_y / 2.0f);
         if ((hx < 1.0f && hy > 5.0f && hy < 15.0f) || (hy < 1.0f && hx > 5.0f && hx < 15.0f))
             frag = F4(0.5f, 0.5f, 0.5f, 0.5f);
     }
-    // frag:859-863
+    return frag;
+}
+
+// frag:859-889: camera ray, flat / percent_black early outs and the initial
+// (u, du) of the geodesic. Returns ST_FLAT, ST_DONE or -1 (integrate).
+__device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const Pix& q, Ray& r) {
+    // full_screen_quad.vert:7-10: uv = NDC of the pixel centre
+    f2 uv = F2((float)(2 * q.px + 1) / (float)fr.width - 1.0f, (float)(2 * q.py + 1) / (float)fr.height - 1.0f);
     f2 uvv = F2(uv.x, uv.y * fr.res_y / fr.res_x);
     m3 cam = ldm(fr.cam_axes);
-    f3 ro = ld3(fr.cam_pos);
-    f3 rd = nrm(mv(cam, F3(uvv.x, uvv.y, fr.ray_forward)));
-    f3 nv = nrm(ro);
-    int steps = 0;
-    int mode;
+    r.ro = ld3(fr.cam_pos);
+    r.rd = nrm(mv(cam, F3(uvv.x, uvv.y, fr.ray_forward)));
+    r.nv = nrm(r.ro);
+    r.steps = 0;
+    r.i = 0;
     const bool flat = fr.raytrace_type == SR_RAYTRACE_FLAT ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_WIDTH && uv.x > 2.0f * fr.curved_percentage + -1.0f) ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_HEIGHT && uv.y > 2.0f * fr.curved_percentage + -1.0f);
-    if (flat || fabsf(dot(rd, nv)) >= 1.0f - SR_EPS) {
-        mode = MODE_FLAT;
-    } else if (fr.percent_black >= 0.0f &&
-               [&] {  // rand(uv_vec) <= percent_black, frag:839-841, 879; rand is in [0, 1)
-                   float x = t_sin(uvv.x * 12.9898f + uvv.y * 78.233f) * 43758.5453f;
-                   return x - floorf(x) <= fr.percent_black;
-               }()) {
-        mode = MODE_DONE;
-    } else {
-        // frag:883-889
-        f3 tv = nrm(cross(cross(nv, rd), nv));
-        float u = 1.0f / len(ro);
-        float du = -u * dot(rd, nv) / dot(rd, tv);
-        mode = MODE_BG;
-        const int N = fr.max_steps;
-        // clearance budget of the polyline since the last anchor (anchor_budget)
-        float T = 0.0f;
-        float B = cull ? anchor_budget(sc, ro) : 0.0f;
-        int i = 0;
-        // Rounds: integrate until this lane's chord hits something (or the ray
-        // ends), shade the wave's pending hits together, and resume the lanes
-        // whose hit was not opaque (frag:930-932) at the next step. Shading
-        // stays out of the step loop's registers and runs once per round.
-        for (;;) {
-            Hit hit = no_hit();
-            for (; i < N; i++) {
-                // {step_size, step_size / 6, cos phi, sin phi} of step i (wave-uniform)
-                const float4 e = tbl[i];
-                steps++;
-                if (u < fr.u_f) {  // frag:891-912
-                    f3 q;
-                    if (!sphere_test(ro, rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) {
-                        mode = MODE_FLAT;
-                        break;
-                    }
-                    nv = nrm(q);
-                    if (fabsf(dot(rd, nv)) >= 1.0f - SR_EPS) {
-                        mode = MODE_FLAT;
-                        break;
-                    }
-                    tv = nrm(cross(cross(nv, rd), nv));
-                    u = 1.0f / len(q);
-                    du = -u * dot(rd, nv) / dot(rd, tv);
-                }
-                // frag:914-919
-                const float h = e.x;
-                {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
-                    float k1 = du;
-                    float l1 = -u * (1.0f - 1.5f * u);
-                    float k2 = du + 0.5f * l1 * h;
-                    float ua = u + 0.5f * k1 * h;
-                    float l2 = -ua * (1.0f - 1.5f * ua);
-                    float k3 = du + 0.5f * l2 * h;
-                    float ub = u + 0.5f * k2 * h;
-                    float l3 = -ub * (1.0f - 1.5f * ub);
-                    float k4 = du + l3 * h;
-                    float uc = u + k3 * h;
-                    float l4 = -uc * (1.0f - 1.5f * uc);
-                    u += e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
-                    du += e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
-                }
-                if (u < 0.0f) break;  // frag:921-922 -> get_bg
-                // frag:924-930
-                f3 prev = ro;
-                ro = (nv * e.z + tv * e.w) / u;
-                f3 delta = ro - prev;
-                float seg = len(delta);
-                rd = delta / seg;
-                T += seg;
-                // wave-uniform: a wave runs the near path if any lane needs it, so
-                // every active lane tests and re-anchors together (keeps the
-                // lanes' anchors in step and the skipped steps coherent)
-#ifdef SR_TIMING_NO_NEAR  // timing experiments only
-                const bool near = false;
-#else
-                const bool near = __ballot(!(T * SR_BUDGET_SLACK < B)) != 0;
-#endif
-                hit = closest_hit(sc, segs, prev, rd, seg, cull, near);
-                if (cull && near) {  // re-anchor at the chord's end
-                    B = anchor_budget(sc, ro);
-                    T = 0.0f;
-                }
-                if (hit.slot != SLOT_NONE) break;
-            }
-            if (hit.slot == SLOT_NONE) break;
-            f4 c = shade(sc, fr, tx, hit, -rd);
-            frag = frag + c;
-            if (c.w == 1.0f) {  // frag:932
-                mode = MODE_DONE;
-                break;
-            }
-            i++;
-        }
+    if (flat || fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return ST_FLAT;
+    if (fr.percent_black >= 0.0f) {  // rand(uv_vec) <= percent_black, frag:839-841, 879; rand is in [0, 1)
+        float x = t_sin(uvv.x * 12.9898f + uvv.y * 78.233f) * 43758.5453f;
+        if (x - floorf(x) <= fr.percent_black) return ST_DONE;
     }
-    if (mode == MODE_FLAT) {
-        f4 c = intersect_color(sc, segs, fr, tx, ro, rd, -1.0f, false, true);
-        frag = frag + c;
-        mode = c.w != 1.0f ? MODE_BG : MODE_DONE;
-    }
-    if (mode == MODE_BG) frag = frag + get_bg(fr, tx, rd);
+    // frag:883-889
+    r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
+    r.u = 1.0f / len(r.ro);
+    r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
+    return -1;
+}
 
-    uint32_t pix = unorm8(frag.x) | (unorm8(frag.y) << 8) | (unorm8(frag.z) << 16) | (unorm8(frag.w) << 24);
-    if (out) *reinterpret_cast<uint32_t*>(out + (size_t)k * pitch + (size_t)px * 4) = pix;
-    if (DEBUG) {
-        size_t i = (size_t)k * (size_t)fr.width + (size_t)px;
-        if (dbg_rgba) {
-            dbg_rgba[4 * i + 0] = frag.x;
-            dbg_rgba[4 * i + 1] = frag.y;
-            dbg_rgba[4 * i + 2] = frag.z;
-            dbg_rgba[4 * i + 3] = frag.w;
+// Where integrate() records translucent hits (sr_integrate_kernel only)
+struct HitLog {
+    PS ps;
+    size_t id;
+    int n;
+};
+
+// The step loop, frag:890-933, from step r.i. Hits that contribute vec4(0)
+// are skipped. RECORD (sr_integrate_kernel): possibly translucent hits are
+// logged and the ray goes on; it stops at an opaque-classified hit (ST_HIT,
+// logged last) or when the log is full (ST_MORE). Otherwise (resume): stops
+// at the first hit not skipped (ST_HIT, in `hit`). r.i = the stopping step.
+// Ends of the ray: ST_FLAT / ST_BG.
+template <bool CULL, bool RECORD>
+__device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                         const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
+                                         Ray& r, Hit& hit, HitLog& log) {
+    Budget bs;
+    if (CULL) budget_init(sc, bs, r.ro);
+    const int N = fr.max_steps;
+    for (; r.i < N; r.i++) {
+        // {step_size, step_size / 6, cos phi, sin phi} of step i (wave-uniform)
+        const float4 e = tbl[r.i];
+        r.steps++;
+        if (r.u < fr.u_f) {  // frag:891-912
+            f3 q;
+            if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
+            r.nv = nrm(q);
+            if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return ST_FLAT;
+            r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
+            r.u = 1.0f / len(q);
+            r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
         }
-        if (dbg_steps) dbg_steps[i] = steps;
+        // frag:914-919
+        const float h = e.x;
+        const float u = r.u, du = r.du;
+        {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
+            float k1 = du;
+            float l1 = -u * (1.0f - 1.5f * u);
+            float k2 = du + 0.5f * l1 * h;
+            float ua = u + 0.5f * k1 * h;
+            float l2 = -ua * (1.0f - 1.5f * ua);
+            float k3 = du + 0.5f * l2 * h;
+            float ub = u + 0.5f * k2 * h;
+            float l3 = -ub * (1.0f - 1.5f * ub);
+            float k4 = du + l3 * h;
+            float uc = u + k3 * h;
+            float l4 = -uc * (1.0f - 1.5f * uc);
+            r.u = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
+            r.du = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
+        }
+        if (r.u < 0.0f) return ST_BG;  // frag:921-922 -> get_bg
+        // frag:924-930
+        f3 prev = r.ro;
+        r.ro = (r.nv * e.z + r.tv * e.w) / r.u;
+        f3 delta = r.ro - prev;
+        float seg = len(delta);
+        r.rd = delta / seg;
+        hit = CULL ? closest_hit_chord(sc, segs, bs, prev, r.rd, seg, r.ro) : closest_hit_all(sc, segs, prev, r.rd, seg);
+        if (hit.slot != SLOT_NONE) {
+            const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
+            if (op == OP_ZERO) continue;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
+            if (!RECORD) return ST_HIT;
+            const int f = PS_HIT0 + PS_HIT_STRIDE * log.n;
+            log.ps.put3(f, log.id, hit.p);
+            log.ps.puti(f + 3, log.id, hit.slot * 8 + hit.face);
+            log.ps.put3(f + 4, log.id, r.rd);
+            log.ps.puti(f + 7, log.id, r.steps);  // the ray's step count if this hit ends it
+            log.n++;
+            if (op == OP_OPAQUE) return ST_HIT;
+            if (log.n == SR_PS_HITS) return ST_MORE;
+        }
+    }
+    return ST_BG;
+}
+
+// The ray's ending (frag:874-876, 895-897, 903-905, 935) after its hits.
+__device__ __forceinline__ void finish_ray(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                           const sr_dev_frame& fr, const Tex& tx, int st, f3 ro, f3 rd, f4& frag) {
+    if (st == ST_FLAT) {
+        f4 c = intersect_color(sc, segs, fr, tx, ro, rd, -1.0f);
+        frag = frag + c;
+        if (c.w == 1.0f) return;
+        st = ST_BG;
+    }
+    if (st == ST_BG) frag = frag + get_bg(fr, tx, rd);
+}
+
+__device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __restrict__ out, size_t pitch,
+                                            float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
+                                            const Pix& q, f4 frag, int steps) {
+    uint32_t pix = unorm8(frag.x) | (unorm8(frag.y) << 8) | (unorm8(frag.z) << 16) | (unorm8(frag.w) << 24);
+    if (out) *reinterpret_cast<uint32_t*>(out + (size_t)q.k * pitch + (size_t)q.px * 4) = pix;
+    const size_t i = (size_t)q.k * (size_t)fr.width + (size_t)q.px;
+    if (dbg_rgba) {
+        dbg_rgba[4 * i + 0] = frag.x;
+        dbg_rgba[4 * i + 1] = frag.y;
+        dbg_rgba[4 * i + 2] = frag.z;
+        dbg_rgba[4 * i + 3] = frag.w;
+    }
+    if (dbg_steps) dbg_steps[i] = steps;
+}
+
+}  // namespace
+
+#ifndef SR_MIN_WAVES_PER_EU
+#define SR_MIN_WAVES_PER_EU 6
+#endif
+
+template <bool CULL>
+__global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
+    const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
+    const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
+    size_t ps_n, int* __restrict__ count) {
+    const int block = blockIdx.y * gridDim.x + blockIdx.x;
+    if (block == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+    Pix q;
+    if (!pixel_of(fr, block, threadIdx.x, q)) return;
+    const size_t id = (size_t)block * 256 + threadIdx.x;
+    Tex tx;
+    tx.bg = nullptr;
+    tx.arr = arr;
+    tx.opq = opq;
+    HitLog log{PS{ps_base, ps_n}, id, 0};
+    const PS& ps = log.ps;
+    Ray r;
+    Hit hit;
+    int st = init_pixel(fr, q, r);
+    if (st < 0) st = integrate<CULL, true>(sc, segs, tbl, fr, tx, r, hit, log);
+    ps.puti(PS_STATUS, id, st);
+    ps.puti(PS_STEPS, id, r.steps);
+    ps.puti(PS_NHITS, id, log.n);
+    ps.put3(PS_RO, id, r.ro);
+    ps.put3(PS_RD, id, r.rd);
+    if (st == ST_HIT || st == ST_MORE) {  // resumable
+        ps.puti(PS_I, id, r.i);
+        ps.put3(PS_NV, id, r.nv);
+        ps.put3(PS_TV, id, r.tv);
+        ps.at(PS_U, id) = r.u;
+        ps.at(PS_DU, id) = r.du;
+    }
+}
+
+__global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __restrict__ sc,
+                                                      const float* __restrict__ segs,
+                                                      const uint32_t* __restrict__ bg,
+                                                      const uint32_t* __restrict__ arr, sr_dev_frame fr,
+                                                      float* __restrict__ ps_base, size_t ps_n,
+                                                      uint8_t* __restrict__ out, size_t pitch,
+                                                      float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
+                                                      int* __restrict__ list, int* __restrict__ count) {
+    const int block = blockIdx.y * gridDim.x + blockIdx.x;
+    Pix q;
+    if (!pixel_of(fr, block, threadIdx.x, q)) return;
+    const size_t id = (size_t)block * 256 + threadIdx.x;
+    const PS ps{ps_base, ps_n};
+    Tex tx;
+    tx.bg = bg;
+    tx.arr = arr;
+    tx.opq = nullptr;
+    const int st = ps.geti(PS_STATUS, id);
+    const int nh = ps.geti(PS_NHITS, id);
+    f4 frag = crosshair_frag(fr, q);
+    bool done = false;
+    int steps_at = -1;
+    for (int j = 0; j < nh && !done; j++) {  // frag:930-932 for each recorded hit, in order
+        const int f = PS_HIT0 + PS_HIT_STRIDE * j;
+        Hit h = no_hit();
+        h.p = ps.get3(f, id);
+        const int key = ps.geti(f + 3, id);
+        h.slot = key >> 3;
+        h.face = key & 7;
+        f4 c = shade(sc, fr, tx, h, -ps.get3(f + 4, id));
+        frag = frag + c;
+        done = c.w == 1.0f;
+        if (done) steps_at = ps.geti(f + 7, id);
+    }
+    if (!done) {
+        if (st == ST_HIT || st == ST_MORE) {
+            // every hit so far translucent, the ray stopped early: accumulate
+            // and queue for sr_resume_kernel
+            ps.put4(PS_FRAG, id, frag);
+            list[atomicAdd(count, 1)] = (int)id;
+            return;
+        }
+        finish_ray(sc, segs, fr, tx, st, ps.get3(PS_RO, id), ps.get3(PS_RD, id), frag);
+    }
+    if (dbg_steps && steps_at < 0) steps_at = ps.geti(PS_STEPS, id);
+    write_pixel(fr, out, pitch, dbg_rgba, dbg_steps, q, frag, steps_at);
+}
+
+template <bool CULL>
+__global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __restrict__ sc,
+                                                       const float4* __restrict__ tbl,
+                                                       const float* __restrict__ segs,
+                                                       const uint32_t* __restrict__ bg,
+                                                       const uint32_t* __restrict__ arr, sr_dev_frame fr,
+                                                       float* __restrict__ ps_base, size_t ps_n,
+                                                       uint8_t* __restrict__ out, size_t pitch,
+                                                       float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
+                                                       const int* __restrict__ list, const int* __restrict__ count) {
+    const int total = *count;
+    const PS ps{ps_base, ps_n};
+    Tex tx;
+    tx.bg = bg;
+    tx.arr = arr;
+    tx.opq = nullptr;
+    for (int w = blockIdx.x * 256 + threadIdx.x; w < total; w += gridDim.x * 256) {
+        const int id = list[w];
+        Pix q;
+        pixel_of(fr, id >> 8, id & 255, q);
+        Ray r;
+        f4 frag = ps.get4(PS_FRAG, id);
+        r.ro = ps.get3(PS_RO, id);
+        r.rd = ps.get3(PS_RD, id);
+        r.nv = ps.get3(PS_NV, id);
+        r.tv = ps.get3(PS_TV, id);
+        r.u = ps.at(PS_U, id);
+        r.du = ps.at(PS_DU, id);
+        r.i = ps.geti(PS_I, id) + 1;
+        r.steps = ps.geti(PS_STEPS, id);
+        HitLog log{ps, (size_t)id, 0};
+        for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
+            Hit hit = no_hit();
+            const int st = integrate<CULL, false>(sc, segs, tbl, fr, tx, r, hit, log);
+            if (st == ST_HIT) {
+                f4 c = shade(sc, fr, tx, hit, -r.rd);
+                frag = frag + c;
+                if (c.w == 1.0f) break;  // frag:932
+                r.i++;
+                continue;
+            }
+            finish_ray(sc, segs, fr, tx, st, r.ro, r.rd, frag);
+            break;
+        }
+        write_pixel(fr, out, pitch, dbg_rgba, dbg_steps, q, frag, r.steps);
     }
 }
 
 extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
-                                         const uint32_t* bg, const uint32_t* arr, const sr_dev_frame* fr,
-                                         uint8_t* out, size_t pitch, float* dbg_rgba, int32_t* dbg_steps,
-                                         hipStream_t stream) {
+                                         const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
+                                         const sr_dev_frame* fr, uint8_t* out, size_t pitch, float* dbg_rgba,
+                                         int32_t* dbg_steps, float* ps, size_t ps_n, int* list, int* count,
+                                         hipEvent_t* ev4, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((fr->width + 15) / 16, (fr->nrows + 15) / 16);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    if (dbg_rgba || dbg_steps)
-        hipLaunchKernelGGL(sr_geodesic_kernel<true>, grid, block, 0, stream, sc, tbl, segs, bg, arr, *fr, out,
-                           pitch, dbg_rgba, dbg_steps);
+    if ((size_t)grid.x * grid.y * 256 > ps_n) return hipErrorInvalidValue;
+    const bool cull = fr->cull != 0;
+    if (ev4) (void)hipEventRecord(ev4[0], stream);
+    if (cull)
+        hipLaunchKernelGGL(sr_integrate_kernel<true>, grid, block, 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n,
+                           count);
     else
-        hipLaunchKernelGGL(sr_geodesic_kernel<false>, grid, block, 0, stream, sc, tbl, segs, bg, arr, *fr, out,
-                           pitch, dbg_rgba, dbg_steps);
+        hipLaunchKernelGGL(sr_integrate_kernel<false>, grid, block, 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n,
+                           count);
+    if (ev4) (void)hipEventRecord(ev4[1], stream);
+    hipLaunchKernelGGL(sr_shade_kernel, grid, block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n, out, pitch, dbg_rgba,
+                       dbg_steps, list, count);
+    if (ev4) (void)hipEventRecord(ev4[2], stream);
+    unsigned nb = grid.x * grid.y < 1024u ? grid.x * grid.y : 1024u;
+    if (cull)
+        hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
+                           out, pitch, dbg_rgba, dbg_steps, list, count);
+    else
+        hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
+                           out, pitch, dbg_rgba, dbg_steps, list, count);
+    if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }

@@ -17,8 +17,10 @@
 #include "sr/sr.h"
 
 extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
-                                         const uint32_t* bg, const uint32_t* arr, const sr_dev_frame* fr,
+                                         const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
+                                         const sr_dev_frame* fr,
                                          uint8_t* out, size_t pitch, float* dbg_rgba, int32_t* dbg_steps,
+                                         float* ps, size_t ps_n, int* list, int* count, hipEvent_t* ev4,
                                          hipStream_t stream);
 
 namespace {
@@ -40,9 +42,22 @@ struct sr_ctx {
     int bg_w = 0, bg_h = 0;
     uint32_t* d_arr = nullptr;
     int arr_w = 0, arr_h = 0, arr_layers = 0;
+    uint8_t* d_opq = nullptr;  // texture-array opacity bitmap (make_opacity_map)
     bool scene_set = false;
     bool cull = true;
     sr_dev_scene h_scene;
+    // pixel pipeline scratch (geodesic.hip): SR_PS_FIELDS planes of ps_n floats,
+    // the resume worklist and its counter; grown on demand, reused per frame.
+    // Renders on one context are ordered on its stream(s) by the caller.
+    float* d_ps = nullptr;
+    int* d_list = nullptr;
+    int* d_count = nullptr;
+    size_t ps_n = 0;
+    // optional per-kernel timing: 4 events per frame (before integrate, after
+    // integrate, after shade, after resume), a ring of `timing_cap` frames
+    std::vector<hipEvent_t> tev;
+    int timing_cap = 0;
+    int timing_n = 0;
     std::map<std::pair<int, int>, Table> tables;  // (max_steps, max_revolutions) -> table
 };
 
@@ -94,6 +109,7 @@ void set_bound(sr_dev_obj& o, V3 c, float R, int kind, float mu) {
     bool planar = o.type == SR_OBJECT_DISK || o.type == SR_OBJECT_HOLLOW_DISK || o.type == SR_OBJECT_RECTANGLE;
     o.mp = planar && std::fabs(dot(n, n) - 1.f) < 1e-5f ? SR_MU_QUADRATIC * (1.f + l1norm(ld(o.f + SR_F_POS)))
                                                          : INFINITY;
+    o.pl1 = l1norm(ld(o.f + SR_F_POS));
 }
 
 void put_transform(float* f, const sr_transform& t) {
@@ -139,7 +155,19 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
     case SR_OBJECT_PLANE:
         if (k < 0 || k >= SR_MAX_PLANES) return SR_E_CAPACITY;
         put_plane(f, s.planes[k]);
-        o.kind = SR_KIND_EXACT;  // unbounded
+        o.kind = SR_KIND_EXACT;
+        {  // unbounded: budgeted by its plane distance alone (rb = +inf)
+            V3 pos = ld(f + SR_F_POS), n = ld(f + SR_F_AXES + 3);
+            if (std::isfinite(l1norm(pos)) && std::fabs(dot(n, n) - 1.f) < 1e-5f) {
+                st(o.bc, pos);
+                o.br = INFINITY;
+                o.rb = INFINITY;
+                o.mu = SR_MU_PLANAR;
+                o.mp = SR_MU_QUADRATIC * (1.f + l1norm(pos));
+                o.pl1 = l1norm(pos);
+                o.kind = SR_KIND_BUDGET;
+            }
+        }
         return SR_OK;
     case SR_OBJECT_DISK: {
         if (k < 0 || k >= SR_MAX_DISKS) return SR_E_CAPACITY;
@@ -165,8 +193,8 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         V3 a0 = ld(f + 3), a1 = ld(f + 6), a2 = ld(f + 9);
         if (orthonormal(a0, a1, a2) && h >= 0.f && r > 0.f) {
             double hh = 0.5 * h;
-            set_bound(o, add(ld(f), scl(a1, (float)hh)), (float)std::sqrt((double)r * r + hh * hh), SR_KIND_CHORD,
-                      SR_MU_PLANAR);
+            set_bound(o, add(ld(f), scl(a1, (float)hh)), (float)std::sqrt((double)r * r + hh * hh),
+                      SR_KIND_BUDGET, SR_MU_PLANAR);
         }
         return SR_OK;
     }
@@ -277,6 +305,68 @@ int upload_rgba(const uint8_t* px, int w, int h, int layers, int ch, uint32_t** 
     return SR_OK;
 }
 
+void free_pixel_state(sr_ctx* ctx) {
+    if (ctx->d_ps) (void)hipFree(ctx->d_ps);
+    if (ctx->d_list) (void)hipFree(ctx->d_list);
+    if (ctx->d_count) (void)hipFree(ctx->d_count);
+    ctx->d_ps = nullptr;
+    ctx->d_list = nullptr;
+    ctx->d_count = nullptr;
+    ctx->ps_n = 0;
+}
+
+int ensure_pixel_state(sr_ctx* ctx, size_t n) {
+    if (n <= ctx->ps_n) return SR_OK;
+    // growing: wait for in-flight frames that use the old buffers
+    if (ctx->ps_n && !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    free_pixel_state(ctx);
+    if (!hip_ok(hipMalloc(&ctx->d_ps, n * SR_PS_FIELDS * sizeof(float))) ||
+        !hip_ok(hipMalloc(&ctx->d_list, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_count, sizeof(int)))) {
+        free_pixel_state(ctx);
+        return SR_E_NOMEM;
+    }
+    ctx->ps_n = n;
+    return SR_OK;
+}
+
+// Opacity bitmap of the texture array for the step loop's hit classification
+// (geodesic.hip hit_opacity): bit (layer, y, x) is set when every texel within
+// +-SR_OPQ_RADIUS of (x, y), wrapping like the sampler, has alpha 255. A
+// bilinear footprint {x0, x0 + 1} x {y0, y0 + 1} whose floor lies within one
+// texel of (x, y) then reads alpha 1 exactly (LERP filtering).
+int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_t** dev) {
+    if (*dev) {
+        (void)hipFree(*dev);
+        *dev = nullptr;
+    }
+    const size_t stride = ((size_t)w + 7) / 8;
+    std::vector<uint8_t> bits(stride * (size_t)h * (size_t)layers, 0);
+    std::vector<uint8_t> row((size_t)w * h);
+    std::vector<uint8_t> tmp((size_t)w * h);
+    const int R = SR_OPQ_RADIUS;
+    for (int l = 0; l < layers; l++) {
+        for (size_t i = 0; i < (size_t)w * h; i++) {
+            const uint8_t* p = px + ((size_t)l * w * h + i) * ch;
+            row[i] = ch == 4 ? (p[3] == 255) : 1;
+        }
+        for (int y = 0; y < h; y++)  // horizontal min, wrapping
+            for (int x = 0; x < w; x++) {
+                uint8_t m = 1;
+                for (int d = -R; d <= R && m; d++) m = row[(size_t)y * w + (((x + d) % w) + w) % w];
+                tmp[(size_t)y * w + x] = m;
+            }
+        for (int y = 0; y < h; y++)  // vertical min, wrapping
+            for (int x = 0; x < w; x++) {
+                uint8_t m = 1;
+                for (int d = -R; d <= R && m; d++) m = tmp[(size_t)((((y + d) % h) + h) % h) * w + x];
+                if (m) bits[((size_t)l * h + y) * stride + (x >> 3)] |= (uint8_t)(1u << (x & 7));
+            }
+    }
+    if (!hip_ok(hipMalloc(dev, bits.size()))) return SR_E_NOMEM;
+    if (!hip_ok(hipMemcpy(*dev, bits.data(), bits.size(), hipMemcpyHostToDevice))) return SR_E_HIP;
+    return SR_OK;
+}
+
 int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
     if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
     if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
@@ -327,8 +417,12 @@ int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
     if (rc != SR_OK) return rc;
-    hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, &fr, out, pitch,
-                                      dbg_rgba, dbg_steps, reinterpret_cast<hipStream_t>(stream));
+    rc = ensure_pixel_state(ctx, (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) * 256);
+    if (rc != SR_OK) return rc;
+    hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
+                                      dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count,
+                                      ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
+                                      reinterpret_cast<hipStream_t>(stream));
     return hip_ok(e) ? SR_OK : SR_E_HIP;
 }
 
@@ -391,7 +485,10 @@ void sr_destroy(sr_ctx* c) {
     if (c->d_segs) (void)hipFree(c->d_segs);
     if (c->d_bg) (void)hipFree(c->d_bg);
     if (c->d_arr) (void)hipFree(c->d_arr);
+    if (c->d_opq) (void)hipFree(c->d_opq);
     for (auto& kv : c->tables) (void)hipFree(kv.second.dev);
+    free_pixel_state(c);
+    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -412,6 +509,7 @@ int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers,
     if (!c || !px || w <= 0 || h <= 0 || layers <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
     if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
     int rc = upload_rgba(px, w, h, layers, ch, &c->d_arr);
+    if (rc == SR_OK) rc = make_opacity_map(px, w, h, layers, ch, &c->d_opq);
     if (rc != SR_OK) {
         c->arr_w = c->arr_h = c->arr_layers = 0;
         return rc;
@@ -432,11 +530,20 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
     std::memset(d.objs, 0, sizeof d.objs);
     d.num_budget = 0;
     d.num_step = 0;
+    d.budget_cyl_mask = 0;
     for (int i = 0; i < s->num_objects; i++) {
         int rc = pack_object(*s, i, d.objs[i]);
         if (rc != SR_OK) return rc;
-        if (d.objs[i].kind == SR_KIND_BUDGET) d.budget_idx[d.num_budget++] = i;
-        else d.step_idx[d.num_step++] = i;
+        sr_dev_obj& o = d.objs[i];
+        // the per-lane budget registers hold SR_MAX_BUDGET objects; further
+        // bounded objects fall back to per-chord bounding-sphere tests
+        if (o.kind == SR_KIND_BUDGET && d.num_budget >= SR_MAX_BUDGET) o.kind = SR_KIND_CHORD;
+        if (o.kind == SR_KIND_BUDGET) {
+            if (o.type == SR_OBJECT_CYLINDER) d.budget_cyl_mask |= 1 << d.num_budget;
+            d.budget_idx[d.num_budget++] = i;
+        } else {
+            d.step_idx[d.num_step++] = i;
+        }
     }
     std::memcpy(d.materials, s->materials, sizeof d.materials);
     std::memcpy(d.lights, s->lights, sizeof d.lights);
@@ -536,6 +643,39 @@ int sr_abi_struct_sizes(size_t* out, int n) {
 int sr_debug_set_culling(sr_ctx* c, int enabled) {
     if (!c) return SR_E_INVALID;
     c->cull = enabled != 0;
+    return SR_OK;
+}
+
+// Not in sr.h's public set: per-kernel HIP-event timing of the next
+// `capacity` frames (0: off). bench.py reads the integrate kernel's duration
+// for its roofline line from here.
+int sr_debug_set_timing(sr_ctx* c, int capacity) {
+    if (!c || capacity < 0 || capacity > (1 << 16)) return SR_E_INVALID;
+    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    c->tev.assign(4 * (size_t)capacity, nullptr);
+    c->timing_cap = 0;
+    c->timing_n = 0;
+    for (auto& e : c->tev)
+        if (!hip_ok(hipEventCreate(&e))) return SR_E_HIP;
+    c->timing_cap = capacity;
+    return SR_OK;
+}
+
+// Waits for the recorded frames and writes ms[3 * f + j] (j = integrate,
+// shade, resume) for up to max_frames of them; *n_frames = frames recorded.
+// Restarts the recording.
+int sr_debug_kernel_times(sr_ctx* c, float* ms, int max_frames, int* n_frames) {
+    if (!c || !n_frames || max_frames < 0 || (max_frames && !ms)) return SR_E_INVALID;
+    *n_frames = c->timing_n;
+    const int n = c->timing_n < max_frames ? c->timing_n : max_frames;
+    for (int f = 0; f < n; f++) {
+        hipEvent_t* e = &c->tev[4 * (size_t)f];
+        if (!hip_ok(hipEventSynchronize(e[3]))) return SR_E_HIP;
+        for (int j = 0; j < 3; j++)
+            if (!hip_ok(hipEventElapsedTime(&ms[3 * f + j], e[j], e[j + 1]))) return SR_E_HIP;
+    }
+    c->timing_n = 0;
     return SR_OK;
 }
 

@@ -49,6 +49,18 @@ class Renderer:
         abi.check(self.lib.sr_debug_set_culling(self.ctx, 1 if enabled else 0), "sr_debug_set_culling")
 
     # ---- rendering -------------------------------------------------------------
+    def set_timing(self, capacity: int) -> None:
+        """Record per-kernel HIP events for the next `capacity` frames (0: off)."""
+        abi.check(self.lib.sr_debug_set_timing(self.ctx, int(capacity)), "sr_debug_set_timing")
+
+    def kernel_times(self, max_frames: int = 4096) -> np.ndarray:
+        """[frames, 3] ms of (integrate, shade, resume) for the recorded frames."""
+        buf = (C.c_float * (3 * max_frames))()
+        n = C.c_int()
+        abi.check(self.lib.sr_debug_kernel_times(self.ctx, buf, max_frames, C.byref(n)), "sr_debug_kernel_times")
+        k = min(n.value, max_frames)
+        return np.frombuffer(buf, dtype=np.float32, count=3 * k).reshape(k, 3).copy()
+
     def _stream(self, stream):
         if stream is None:
             stream = self.torch.cuda.current_stream(self.tdev)
