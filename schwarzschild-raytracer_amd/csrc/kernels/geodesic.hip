@@ -314,64 +314,67 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // Per-lane budget state: E[j] = clearance_j(anchor_j) - slacked path from
 // anchor_j to the last budget event, T = slacked path since that event,
 // m = min_j E[j]. Slots re-anchor independently: only those whose budget is
-// spent are tested and re-anchored.
+// spent are tested and re-anchored. Unused slots hold +inf.
 struct Budget {
     float E[SR_MAX_BUDGET + 1];
     float T, m;
 };
 
+// E[j] = v for a wave-uniform slot j (constant register indices: no scratch)
+__device__ __forceinline__ void budget_set(Budget& bs, int j, float v) {
+#pragma unroll
+    for (int jj = 0; jj <= SR_MAX_BUDGET; jj++)
+        if (jj == j) bs.E[jj] = v;
+}
+
+__device__ __forceinline__ float budget_min(const Budget& bs) {
+    float m = bs.E[0];
+#pragma unroll
+    for (int j = 1; j <= SR_MAX_BUDGET; j++) m = nmin(m, bs.E[j]);
+    return m;
+}
+
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
-    bs.m = INFINITY;
 #pragma unroll
-    for (int j = 0; j <= SR_MAX_BUDGET; j++) {
-        if (j <= nb) {
-            bs.E[j] = clearance(sc, j, A, a);
-            bs.m = nmin(bs.m, bs.E[j]);
-        }
-    }
+    for (int j = 0; j <= SR_MAX_BUDGET; j++) bs.E[j] = INFINITY;
+#pragma unroll 1
+    for (int j = 0; j <= nb; j++) budget_set(bs, j, clearance(sc, j, A, a));
+    bs.m = budget_min(bs);
 }
 
-// Intersect objects[] and the black hole in budget slots with the chord
-// [o, o + seg*d] (ending at `end`) where the budget requires it, and advance
-// the budgets. The branch structure is wave-uniform (ballots).
-__device__ __forceinline__ void budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, Hit& best, f3 o, f3 d,
-                                            float seg, float S, f3 end) {
+// Advance the budgets over the chord [o, o + seg*d] ending at `end`. Returns
+// the wave-uniform mask of slots whose exact test this chord needs (bit 0:
+// the black hole, bit j: objs[budget_idx[j - 1]]); those slots re-anchor at
+// `end`. The branch structure is wave-uniform (ballots).
+__device__ __forceinline__ uint32_t budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 d, float seg,
+                                                f3 end) {
     bs.T += seg * SR_PATH_SLACK;
     bool fire = !(bs.T < bs.m);
-    const int nb = sc->num_budget;
-    const int cm = sc->budget_cyl_mask;
-    if (cm) {
+    const uint32_t cm = (uint32_t)sc->budget_cyl_mask;
+    for (uint32_t c = cm; c; c &= c - 1) fire = fire || budget_parallel(sc, __builtin_ctz(c) + 1, d);
+    if (!__ballot(fire)) return 0u;
+    uint32_t need = 0;
 #pragma unroll
-        for (int j = 1; j <= SR_MAX_BUDGET; j++) {
-            if (j <= nb) fire = fire || budget_parallel(sc, j, d);
-        }
+    for (int j = 0; j <= SR_MAX_BUDGET; j++)
+        if (__ballot(!(bs.T < bs.E[j]))) need |= 1u << j;
+    for (uint32_t c = cm; c; c &= c - 1) {
+        const int j = __builtin_ctz(c) + 1;
+        if (__ballot(budget_parallel(sc, j, d))) need |= 1u << j;
     }
-    if (!__ballot(fire)) return;
-    const float a = __builtin_amdgcn_sqrtf(dot(end, end));
-    float m = INFINITY;
 #pragma unroll
-    for (int j = 0; j <= SR_MAX_BUDGET; j++) {
-        if (j > nb) continue;
-        if (__ballot(!(bs.T < bs.E[j]) || budget_parallel(sc, j, d))) {
-            f3 p;
-            if (j == 0) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
-                consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, seg, p), p, o, SLOT_BH, 0, KEY_BH);
-            } else {
-                const int k = sc->budget_idx[j - 1];
-                const sr_dev_obj& ob = sc->objs[k];
-                if (may_hit(ob, o, d, seg, S)) test_object(best, ob, k, o, d, seg);
-            }
-            bs.E[j] = clearance(sc, j, end, a);
-        } else {
-            bs.E[j] = bs.E[j] - bs.T;
-        }
-        m = nmin(m, bs.E[j]);
+    for (int j = 0; j <= SR_MAX_BUDGET; j++)
+        if (!((need >> j) & 1u)) bs.E[j] = bs.E[j] - bs.T;
+    const float a = __builtin_amdgcn_sqrtf(dot(end, end));
+    for (uint32_t c = need; c; c &= c - 1) {
+        const int j = __builtin_ctz(c);
+        budget_set(bs, j, clearance(sc, j, end, a));
     }
     bs.T = 0.0f;
-    bs.m = m;
+    bs.m = budget_min(bs);
+    return need;
 }
 
 // The test rays (frag:760-803), visited right after the black hole.
@@ -406,25 +409,34 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 
 // intersect() for one chord of the step loop with culling: the test rays, the
 // objects tested every step (chord-culled ones only when the chord reaches
-// their bounding sphere), then the budget slots. Same winner as
-// closest_hit_all (lexicographic keys, skipped tests provably miss).
+// their bounding sphere) and the budget slots whose budget is spent. Same
+// winner as closest_hit_all (lexicographic keys, skipped tests provably
+// miss). One copy of each exact test: the candidates are collected into a
+// wave-uniform object mask first.
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                                  Budget& bs, f3 o, f3 d, float seg, f3 end) {
     Hit best = no_hit();
     test_ray_hits(sc, segs, best, o, d, seg);
-    const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;
-#ifdef SR_TIMING_NO_STEPOBJ  // timing experiments only
-    const int ns = 0;
-#else
+    uint32_t om = 0;  // objects to test (wave-uniform)
+#ifndef SR_TIMING_NO_STEPOBJ  // timing experiments only
     const int ns = sc->num_step;
+    for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
 #endif
-    for (int j = 0; j < ns; j++) {
-        const int k = sc->step_idx[j];
-        const sr_dev_obj& ob = sc->objs[k];
-        if (ob.kind == SR_KIND_CHORD && !may_hit(ob, o, d, seg, S)) continue;
-        test_object(best, ob, k, o, d, seg);
+    const uint32_t need = budget_step(sc, bs, d, seg, end);
+    if (need & 1u) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
+        f3 p;
+        consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, seg, p), p, o, SLOT_BH, 0, KEY_BH);
     }
-    budget_step(sc, bs, best, o, d, seg, S, end);
+    for (uint32_t c = need >> 1; c; c &= c - 1) om |= 1u << sc->budget_idx[__builtin_ctz(c)];
+    if (om) {
+        const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;
+        for (; om; om &= om - 1) {
+            const int k = __builtin_ctz(om);
+            const sr_dev_obj& ob = sc->objs[k];
+            if (ob.kind != SR_KIND_EXACT && !may_hit(ob, o, d, seg, S)) continue;
+            test_object(best, ob, k, o, d, seg);
+        }
+    }
     return best;
 }
 
