@@ -79,6 +79,20 @@ struct Tex {
     const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
+#ifdef SR_STATS
+// Measurement builds only: wave-level event counters (tools/stats_frame.py).
+//   0 wave-steps  1 fired wave-steps  2..10 slot j tested  11 fired by the
+//   parallel / forced rule only  12 exact object tests run  13 lane-steps
+__device__ unsigned long long sr_stats[32];
+__device__ __forceinline__ void stat_add(int k, unsigned long long v) {
+    const unsigned long long act = __ballot(1);
+    if ((int)__lane_id() == __builtin_ctzll(act)) atomicAdd(&sr_stats[k], v);
+}
+#define SR_STAT(k, v) stat_add(k, v)
+#else
+#define SR_STAT(k, v) ((void)0)
+#endif
+
 // ---- primitive tests: return the reference's is_hit and fill p ------------
 // sphere_intersect, frag:457-478
 __device__ __forceinline__ bool sphere_test(f3 o, f3 d, f3 c, float r, float max_lambda, f3& p) {
@@ -318,6 +332,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 struct Budget {
     float E[SR_MAX_BUDGET + 1];
     float T, m;
+#ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
+    int fires;
+#endif
 };
 
 // E[j] = v for a wave-uniform slot j (constant register indices: no scratch)
@@ -345,17 +362,12 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     bs.m = budget_min(bs);
 }
 
-// Advance the budgets over the chord [o, o + seg*d] ending at `end`. Returns
-// the wave-uniform mask of slots whose exact test this chord needs (bit 0:
-// the black hole, bit j: objs[budget_idx[j - 1]]); those slots re-anchor at
-// `end`. The branch structure is wave-uniform (ballots).
-__device__ __forceinline__ uint32_t budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 d, float seg,
-                                                f3 end) {
-    bs.T += seg * SR_PATH_SLACK;
-    bool fire = !(bs.T < bs.m);
+// Budget event for the chord ending at `end` with direction d (bs.T already
+// includes the chord). Returns the wave-uniform mask of slots whose exact test
+// this chord needs (bit 0: the black hole, bit j: objs[budget_idx[j - 1]]);
+// those slots re-anchor at `end`, the others are charged bs.T.
+__device__ __forceinline__ uint32_t budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 d, f3 end) {
     const uint32_t cm = (uint32_t)sc->budget_cyl_mask;
-    for (uint32_t c = cm; c; c &= c - 1) fire = fire || budget_parallel(sc, __builtin_ctz(c) + 1, d);
-    if (!__ballot(fire)) return 0u;
     uint32_t need = 0;
 #pragma unroll
     for (int j = 0; j <= SR_MAX_BUDGET; j++)
@@ -418,11 +430,15 @@ __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict_
     Hit best = no_hit();
     test_ray_hits(sc, segs, best, o, d, seg);
     uint32_t om = 0;  // objects to test (wave-uniform)
-#ifndef SR_TIMING_NO_STEPOBJ  // timing experiments only
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
+    const uint32_t need = budget_step(sc, bs, d, end);
+#ifdef SR_STATS
+    for (uint32_t c = need; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
 #endif
-    const uint32_t need = budget_step(sc, bs, d, seg, end);
+#ifdef SR_STATS_FIRE
+    bs.fires += (need != 0u || om != 0u) ? 1 : 0;
+#endif
     if (need & 1u) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
         f3 p;
         consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, seg, p), p, o, SLOT_BH, 0, KEY_BH);
@@ -434,10 +450,48 @@ __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict_
             const int k = __builtin_ctz(om);
             const sr_dev_obj& ob = sc->objs[k];
             if (ob.kind != SR_KIND_EXACT && !may_hit(ob, o, d, seg, S)) continue;
+            SR_STAT(12, 1);
             test_object(best, ob, k, o, d, seg);
         }
     }
     return best;
+}
+
+// Upper bound of the exact chord length |ro_i - ro_(i-1)| from the orbit
+// alone (no divisions): both points are (nv cos phi + tv sin phi) / u, so
+// dv = nv (rB cB - rA cA) + tv (rB sB - rA sA) with r = 1/u approximates the
+// chord to ~1.4e-6 (rA + rB) absolute (rounding of the reference's float
+// evaluation of both points); the bound adds 8e-6 (rA + rB) and
+// a relative 1e-4 for the approximate rcp / sqrt.
+struct ChordBound {
+    f3 dv;
+    float dd, len, abs_err;
+};
+__device__ __forceinline__ ChordBound chord_bound(f3 nv, f3 tv, float rA, float rB, float cA, float sA, float cB,
+                                                  float sB) {
+    ChordBound b;
+    const float a = rB * cB - rA * cA, c = rB * sB - rA * sA;
+    b.dv = nv * a + tv * c;
+    b.dd = dot(b.dv, b.dv);
+    b.abs_err = 8.0e-6f * (rA + rB);
+    b.len = __builtin_amdgcn_sqrtf(b.dd) * 1.0001f + b.abs_err;
+    return b;
+}
+
+// Whether a budgeted cylinder may see this chord closer than SR_BUDGET_DPMIN
+// to its axis direction (then the exact chord must be tested): decided on the
+// approximate direction dv with twice the threshold, and forced when dv is
+// not known to 0.4%.
+__device__ __forceinline__ bool chord_near_parallel(const sr_dev_scene* __restrict__ sc, const ChordBound& b) {
+    const uint32_t cm = (uint32_t)sc->budget_cyl_mask;
+    if (!cm) return false;
+    bool par = !(b.abs_err <= 0.004f * __builtin_amdgcn_sqrtf(b.dd));
+    for (uint32_t c = cm; c; c &= c - 1) {
+        const sr_dev_obj& ob = sc->objs[sc->budget_idx[__builtin_ctz(c)]];
+        const float ca = dot(b.dv, ld3(ob.f + SR_F_AXES + 3));
+        par = par || !(b.dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * b.dd);
+    }
+    return par;
 }
 
 // ---- textures ------------------------------------------------
@@ -954,24 +1008,72 @@ struct HitLog {
     int n;
 };
 
-// The step loop, frag:890-933, from step r.i. Hits that contribute vec4(0)
-// are skipped. RECORD (sr_integrate_kernel): possibly translucent hits are
-// logged and the ray goes on; it stops at an opaque-classified hit (ST_HIT,
-// logged last) or when the log is full (ST_MORE). Otherwise (resume): stops
-// at the first hit not skipped (ST_HIT, in `hit`). r.i = the stopping step.
-// Ends of the ray: ST_FLAT / ST_BG.
+// Chord end point of step j, frag:924: (nv cos phi_j + tv sin phi_j) / u_j
+__device__ __forceinline__ f3 point_at(const Ray& r, float u, float c, float s) { return (r.nv * c + r.tv * s) / u; }
+
+// The step loop, frag:890-933, from step r.i (entry: r.u = u after step
+// r.i - 1, r.ro / r.rd = that step's chord end and direction).
+//
+// Lazy chords (CULL): the reference computes every chord exactly (two
+// divisions by u, a sqrt and three divisions by its length); here a step
+// whose chord provably cannot hit anything only advances (u, du) and charges
+// the clearance budgets an upper bound of its length (chord_bound). The wave
+// materialises the exact chord - the reference's float expressions on the same
+// operands, so bit-identical - when any lane's budget is spent or its chord may
+// be near-parallel to a budgeted cylinder, and at every exit and reseed.
+//
+// Hits that contribute vec4(0) are skipped. RECORD (sr_integrate_kernel):
+// possibly translucent hits are logged and the ray goes on; it stops at an
+// opaque-classified hit (ST_HIT, logged last) or when the log is full
+// (ST_MORE). Otherwise (resume): stops at the first hit not skipped (ST_HIT,
+// in `hit`). r.i = the stopping step. Ends of the ray: ST_FLAT / ST_BG.
 template <bool CULL, bool RECORD>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
     Budget bs;
     if (CULL) budget_init(sc, bs, r.ro);
+#ifdef SR_STATS_FIRE
+    bs.fires = 0;
+    struct Out {
+        Ray& r;
+        Budget& b;
+        __device__ ~Out() { r.steps = b.fires; }
+    } out_{r, bs};
+#endif
     const int N = fr.max_steps;
+    // Chord bookkeeping: im = the step whose chord r.ro / r.rd hold; up = u
+    // after step i - 2; (c1, s1) / (c2, s2) = cos / sin phi of steps i - 1 /
+    // i - 2 (step -1: the camera, phi = 0); rA ~ 1 / u after step i - 1.
+    int im = r.i - 1;
+    float up = 0.0f;
+    float c1 = 1.0f, s1 = 0.0f, c2 = 1.0f, s2 = 0.0f;
+    if (r.i > 0) {
+        const float4 e1 = tbl[r.i - 1];
+        c1 = e1.z;
+        s1 = e1.w;
+    }
+    float rA = __builtin_amdgcn_rcpf(r.u);
+    // materialise the chord of step i - 1 (its end point from r.u, its start
+    // from r.ro when that is step i - 2, else from up)
+    auto settle_prev = [&](int i) {
+        if (im == i - 1) return;
+        f3 A = im == i - 2 ? r.ro : point_at(r, up, c2, s2);
+        f3 B = point_at(r, r.u, c1, s1);
+        f3 delta = B - A;
+        float seg = len(delta);
+        r.rd = delta / seg;
+        r.ro = B;
+        im = i - 1;
+    };
     for (; r.i < N; r.i++) {
+        const int i = r.i;
         // {step_size, step_size / 6, cos phi, sin phi} of step i (wave-uniform)
-        const float4 e = tbl[r.i];
+        const float4 e = tbl[i];
         r.steps++;
+        bool force = !CULL;
         if (r.u < fr.u_f) {  // frag:891-912
+            settle_prev(i);
             f3 q;
             if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
             r.nv = nrm(q);
@@ -979,10 +1081,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
             r.u = 1.0f / len(q);
             r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
+            force = true;  // new orbital frame: this chord is materialised exactly
         }
         // frag:914-919
         const float h = e.x;
         const float u = r.u, du = r.du;
+        float un, dun;
         {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
             float k1 = du;
             float l1 = -u * (1.0f - 1.5f * u);
@@ -995,17 +1099,51 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             float k4 = du + l3 * h;
             float uc = u + k3 * h;
             float l4 = -uc * (1.0f - 1.5f * uc);
-            r.u = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
-            r.du = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
+            un = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
+            dun = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
         }
-        if (r.u < 0.0f) return ST_BG;  // frag:921-922 -> get_bg
-        // frag:924-930
-        f3 prev = r.ro;
-        r.ro = (r.nv * e.z + r.tv * e.w) / r.u;
+        if (un < 0.0f) {  // frag:921-922 -> get_bg with the previous chord
+            settle_prev(i);
+            return ST_BG;
+        }
+        float rB = 0.0f;
+        const bool bounded = CULL && !force;  // this chord's length is charged below, else when exact
+        if (bounded) {
+            rB = __builtin_amdgcn_rcpf(un);
+            const ChordBound cb = chord_bound(r.nv, r.tv, rA, rB, c1, s1, e.z, e.w);
+            bs.T += cb.len * SR_PATH_SLACK;
+            force = !(bs.T < bs.m) || chord_near_parallel(sc, cb);
+#ifdef SR_STATS
+            SR_STAT(11, __ballot(force) && !__ballot(!(bs.T < bs.m)) ? 1 : 0);
+#endif
+        }
+        SR_STAT(0, 1);
+        SR_STAT(13, __popcll(__ballot(1)));
+        // advance: step i's u becomes the current one
+        up = r.u;
+        r.u = un;
+        r.du = dun;
+        c2 = c1;
+        s2 = s1;
+        c1 = e.z;
+        s1 = e.w;
+        rA = rB;
+        if (!__ballot(force)) continue;
+        SR_STAT(1, 1);
+        // frag:924-930: the exact chord of step i
+        f3 prev = im == i - 1 ? r.ro : point_at(r, up, c2, s2);
+        r.ro = point_at(r, r.u, e.z, e.w);
+        im = i;
         f3 delta = r.ro - prev;
         float seg = len(delta);
         r.rd = delta / seg;
-        hit = CULL ? closest_hit_chord(sc, segs, bs, prev, r.rd, seg, r.ro) : closest_hit_all(sc, segs, prev, r.rd, seg);
+        rA = __builtin_amdgcn_rcpf(r.u);
+        if (CULL) {
+            if (!bounded) bs.T += seg * SR_PATH_SLACK;
+            hit = closest_hit_chord(sc, segs, bs, prev, r.rd, seg, r.ro);
+        } else {
+            hit = closest_hit_all(sc, segs, prev, r.rd, seg);
+        }
         if (hit.slot != SLOT_NONE) {
             const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
             if (op == OP_ZERO) continue;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
@@ -1020,6 +1158,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             if (log.n == SR_PS_HITS) return ST_MORE;
         }
     }
+    settle_prev(r.i);
     return ST_BG;
 }
 
@@ -1053,7 +1192,7 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 }  // namespace
 
 #ifndef SR_MIN_WAVES_PER_EU
-#define SR_MIN_WAVES_PER_EU 6
+#define SR_MIN_WAVES_PER_EU 5
 #endif
 
 template <bool CULL>
@@ -1217,3 +1356,14 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }
+
+#ifdef SR_STATS
+// Measurement builds only: read (and clear) the kernel's event counters.
+extern "C" int sr_debug_stats(unsigned long long* out32) {
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
+    unsigned long long z[32] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z) != hipSuccess) return -3;
+    return 0;
+}
+#endif

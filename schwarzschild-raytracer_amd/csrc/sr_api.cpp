@@ -321,7 +321,7 @@ int ensure_pixel_state(sr_ctx* ctx, size_t n) {
     if (ctx->ps_n && !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
     free_pixel_state(ctx);
     if (!hip_ok(hipMalloc(&ctx->d_ps, n * SR_PS_FIELDS * sizeof(float))) ||
-        !hip_ok(hipMalloc(&ctx->d_list, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_count, sizeof(int)))) {
+        !hip_ok(hipMalloc(&ctx->d_list, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_count, 2 * sizeof(int)))) {
         free_pixel_state(ctx);
         return SR_E_NOMEM;
     }

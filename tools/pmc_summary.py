@@ -7,7 +7,7 @@ import json
 import sys
 
 
-def summarise(root, kernel="sr_geodesic_kernel<false>"):
+def summarise(root, kernel="sr_integrate_kernel<true>"):
     out = {}
     for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         agg = collections.defaultdict(float)

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Event counters of an SR_STATS build (tools/build_variant.sh NAME -DSR_STATS):
+renders the headline frame once and prints the step loop's wave-level counts.
+  python tools/stats_frame.py lib/variants/libsr_NAME.so [--scene tex|untex|bh]"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+NAMES = {0: "wave_steps", 1: "fired", 11: "fired_parallel_only", 12: "object_tests", 13: "lane_steps"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib")
+    ap.add_argument("--scene", default="tex")
+    ap.add_argument("--max-steps", type=int, default=2000)
+    args = ap.parse_args()
+    os.environ["SR_LIB"] = str(Path(args.lib).resolve())
+    import torch  # noqa: F401  (HIP runtime up before the library)
+
+    import srpkg
+
+    pkg = srpkg.load_package()
+    abi, sc = pkg.abi, pkg.scenes
+    lib = abi.load()
+    lib.sr_debug_stats.restype = C.c_int
+    lib.sr_debug_stats.argtypes = [C.POINTER(C.c_ulonglong)]
+    r = pkg.Renderer(0)
+    if args.scene == "bh":
+        r.set_scene(sc.scene_black_hole_only())
+    else:
+        r.set_scene(sc.scene_default(textured=args.scene == "tex"))
+    r.set_background(sc.skybox(2048, 1024))
+    arr, _, _ = sc.default_texture_array()
+    r.set_texture_array(arr)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=args.max_steps, percent_black=-1.0)
+    buf = (C.c_ulonglong * 32)()
+    lib.sr_debug_stats(buf)  # clear
+    r.render(cam, params, 1920, 1080)
+    assert lib.sr_debug_stats(buf) == 0
+    out = {NAMES.get(k, f"slot{k - 2}_tested" if 2 <= k <= 10 else str(k)): int(buf[k]) for k in range(14)}
+    out["fired_frac"] = out["fired"] / max(1, out["wave_steps"])
+    print(json.dumps(out, indent=1))
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
