@@ -66,7 +66,7 @@ typedef struct {
     float br;        // bounding-sphere radius + static margin (per-chord test)
     float rb;        // budget radius: br + SR_MU_QUADRATIC * (1 + |bc|_1 + br)
     float mu;        // per-chord margin factor (SR_MU_*)
-    float mp;        // planar objects: plane-distance margin SR_MU_QUADRATIC * (1 + |pos|_1), else +inf
+    float mp;        // distance-to-primitive margin SR_MU_QUADRATIC * (1 + |pos|_1 + R), +inf: bounding sphere only
     float pl1;       // |pos|_1 (cylinder margins scale with |o - pos|)
     float f[SR_OBJ_FLOATS - 4];
 } sr_dev_obj;  // 512 B

@@ -84,11 +84,18 @@ struct Tex {
 //   0 wave-steps  1 fired wave-steps  2..10 slot j tested  11 fired by the
 //   parallel / forced rule only  12 exact object tests run  13 lane-steps
 __device__ unsigned long long sr_stats[32];
+// per-wave [start, end] s_memrealtime (100 MHz) of sr_integrate_kernel, by wave index
+#define SR_WAVE_LOG (1 << 17)
+__device__ unsigned long long sr_wave_t[2 * SR_WAVE_LOG];
 __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
     const unsigned long long act = __ballot(1);
     if ((int)__lane_id() == __builtin_ctzll(act)) atomicAdd(&sr_stats[k], v);
 }
+#ifdef SR_STATS_NOCOUNT  // timeline only: the counters' atomics distort it
+#define SR_STAT(k, v) ((void)0)
+#else
 #define SR_STAT(k, v) stat_add(k, v)
+#endif
 #else
 #define SR_STAT(k, v) ((void)0)
 #endif
@@ -300,11 +307,36 @@ __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, 
         const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
         f3 w = A - ld3(ob.bc);
         c = __builtin_amdgcn_sqrtf(dot(w, w)) - ob.rb;
-        if (ob.type == SR_OBJECT_PLANE || ob.type == SR_OBJECT_DISK || ob.type == SR_OBJECT_HOLLOW_DISK ||
-            ob.type == SR_OBJECT_RECTANGLE) {
-            f3 q = A - ld3(ob.f + SR_F_POS);
-            c = fmaxf(c, fabsf(dot(q, ld3(ob.f + SR_F_AXES + 3))) - ob.mp);
-        } else if (ob.type == SR_OBJECT_CYLINDER) {
+        if (ob.mp < INFINITY) {  // distance to the primitive itself (orthonormal frame)
+            const float* f = ob.f;
+            const f3 q = A - ld3(f + SR_F_POS);
+            const float y = dot(q, ld3(f + SR_F_AXES + 3));  // along axes[1] (plane normal / height)
+            float d2;
+            if (ob.type == SR_OBJECT_PLANE) {
+                d2 = y * y;
+            } else if (ob.type == SR_OBJECT_RECTANGLE || ob.type == SR_OBJECT_BOX) {
+                const float x = dot(q, ld3(f + SR_F_AXES)), z = dot(q, ld3(f + SR_F_AXES + 6));
+                const bool box = ob.type == SR_OBJECT_BOX;
+                const float wx = box ? f[12] : f[17], wz = box ? f[13] : f[18];
+                const float ex = fmaxf(0.0f, fmaxf(-x, x - wx)), ez = fmaxf(0.0f, fmaxf(-z, z - wz));
+                const float ey = box ? fmaxf(0.0f, fmaxf(-y, y - f[14])) : y;
+                d2 = ex * ex + ey * ey + ez * ez;
+            } else {  // disk, hollow disk, cylinder: radial distance from axes[1]
+                const float rho = __builtin_amdgcn_sqrtf(fmaxf(0.0f, dot(q, q) - y * y));
+                float er, ey = y;
+                if (ob.type == SR_OBJECT_DISK) {
+                    er = fmaxf(0.0f, rho - f[17]);
+                } else if (ob.type == SR_OBJECT_HOLLOW_DISK) {
+                    er = fmaxf(0.0f, fmaxf(f[17] - rho, rho - f[18]));
+                } else {
+                    er = fmaxf(0.0f, rho - f[SR_F_P0 + 1]);
+                    ey = fmaxf(0.0f, fmaxf(-y, y - f[SR_F_P0]));
+                }
+                d2 = er * er + ey * ey;
+            }
+            c = fmaxf(c, __builtin_amdgcn_sqrtf(d2) - ob.mp);
+        }
+        if (ob.type == SR_OBJECT_CYLINDER) {
             float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + ob.pl1 + (3.0f * SR_BUDGET_TMAX + 1.0f);
             float qm = SR_CYL_QMARGIN * Sb * Sb / (ob.f[SR_F_P0 + 1] * SR_BUDGET_DPMIN);
             c = fminf(c - qm, SR_BUDGET_TMAX);
@@ -313,25 +345,19 @@ __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, 
     return c - 1.8f * SR_MU_QUADRATIC * a;
 }
 
-// A budgeted cylinder's window margin holds only for chords whose direction
-// keeps |d_perp|^2 >= SR_BUDGET_DPMIN; others are tested regardless.
-__device__ __forceinline__ bool budget_parallel(const sr_dev_scene* __restrict__ sc, int j, f3 d) {
-    if (j == 0 || !((sc->budget_cyl_mask >> (j - 1)) & 1)) return false;
-    const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
-    float ca = dot(d, ld3(ob.f + SR_F_AXES + 3));
-    return !(1.0f - ca * ca >= SR_BUDGET_DPMIN);
-}
-
 // NaN-propagating minimum: a NaN clearance must force the exact tests.
 __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e : m; }
 
 // Per-lane budget state: E[j] = clearance_j(anchor_j) - slacked path from
 // anchor_j to the last budget event, T = slacked path since that event,
 // m = min_j E[j]. Slots re-anchor independently: only those whose budget is
-// spent are tested and re-anchored. Unused slots hold +inf.
+// spent are re-anchored (and tested if the chord may reach them). Unused
+// slots hold +inf. (pa, pb)[k] = (nv, tv) . axis of the k-th budgeted
+// cylinder (budget_cyl_mask bit order) for the chord-direction test.
 struct Budget {
     float E[SR_MAX_BUDGET + 1];
     float T, m;
+    float pa[SR_MAX_CYLINDERS], pb[SR_MAX_CYLINDERS];
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -351,7 +377,21 @@ __device__ __forceinline__ float budget_min(const Budget& bs) {
     return m;
 }
 
-__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A) {
+// the orbital frame's projections on the budgeted cylinders' axes
+__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 nv, f3 tv) {
+    uint32_t c = (uint32_t)sc->budget_cyl_mask;
+#pragma unroll
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        if (c) {
+            const f3 ax = ld3(sc->objs[sc->budget_idx[__builtin_ctz(c)]].f + SR_F_AXES + 3);
+            bs.pa[k] = dot(nv, ax);
+            bs.pb[k] = dot(tv, ax);
+            c &= c - 1;
+        }
+    }
+}
+
+__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
@@ -360,33 +400,100 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 #pragma unroll 1
     for (int j = 0; j <= nb; j++) budget_set(bs, j, clearance(sc, j, A, a));
     bs.m = budget_min(bs);
+    budget_frame(sc, bs, nv, tv);
 }
 
-// Budget event for the chord ending at `end` with direction d (bs.T already
-// includes the chord). Returns the wave-uniform mask of slots whose exact test
-// this chord needs (bit 0: the black hole, bit j: objs[budget_idx[j - 1]]);
-// those slots re-anchor at `end`, the others are charged bs.T.
-__device__ __forceinline__ uint32_t budget_step(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 d, f3 end) {
-    const uint32_t cm = (uint32_t)sc->budget_cyl_mask;
-    uint32_t need = 0;
+// Whether the chord with in-plane components (a, b) (chord = nv a + tv b, up
+// to perr absolute) may be closer than SR_BUDGET_DPMIN to a budgeted
+// cylinder's axis direction; bit k of the result: cylinder k (bit order of
+// budget_cyl_mask). Decided with twice the threshold and forced when the
+// direction is not known to 0.4%.
+__device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restrict__ sc, const Budget& bs, float a,
+                                                   float b, float perr) {
+    uint32_t c = (uint32_t)sc->budget_cyl_mask;
+    if (!c) return 0u;
+    const float dd = a * a + b * b;
+    const bool vague = !(perr * perr <= 1.6e-5f * dd);
+    uint32_t par = 0;
+#pragma unroll
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        if (c) {
+            const float ca = a * bs.pa[k] + b * bs.pb[k];
+            if (vague || !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd)) par |= 1u << k;
+            c &= c - 1;
+        }
+    }
+    return par;
+}
+
+// Conservative: may the exact chord, within perr of the segment [A, B], come
+// within reach of slot j's exact test (per-chord margins of may_hit)?
+__device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ sc, int j, f3 A, f3 B, float perr) {
+    const f3 dv = B - A;
+    const float dd = dot(dv, dv);
+    const float len = __builtin_amdgcn_sqrtf(dd);
+    const float S = ((fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + len + 1.0f) * 1.001f + perr;
+    f3 c;
+    float R;
+    if (j == 0) {
+        c = F3(0.0f, 0.0f, 0.0f);
+        R = 1.0f + SR_MU_QUADRATIC * S;  // the black hole: sphere r = 1 at the origin
+    } else {
+        const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
+        c = ld3(ob.bc);
+        R = ob.br + ob.mu * S;
+        if (ob.type == SR_OBJECT_CYLINDER) {
+            const float ca = dot(dv, ld3(ob.f + SR_F_AXES + 3));
+            const float dp = (dd - ca * ca) * __builtin_amdgcn_rcpf(dd) * 0.5f;
+            const float r = ob.f[SR_F_P0 + 1];
+            if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
+            const float Sc = S + ob.pl1;
+            R = R + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp);
+        }
+    }
+    R = R * 1.001f + perr;
+    const f3 w = c - A;
+    float t = dot(w, dv) * __builtin_amdgcn_rcpf(dd);
+    t = t > 0.0f ? t : 0.0f;  // NaN -> 0
+    t = t < 1.0f ? t : 1.0f;
+    const f3 q = w - dv * t;
+    return !(dot(q, q) > R * R);
+}
+
+// Budget event for the chord of this step, known approximately as [A, B]
+// (exact end points within perr; bs.T already charged with it). Slots whose
+// budget is spent, or cylinders the chord may be near-parallel to (par),
+// re-anchor at B (clearance - perr); returns the wave-uniform mask of those
+// the chord may reach: their exact tests need the exact chord.
+__device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
+                                                 float perr, uint32_t par) {
+    uint32_t spent = 0;
 #pragma unroll
     for (int j = 0; j <= SR_MAX_BUDGET; j++)
-        if (__ballot(!(bs.T < bs.E[j]))) need |= 1u << j;
-    for (uint32_t c = cm; c; c &= c - 1) {
-        const int j = __builtin_ctz(c) + 1;
-        if (__ballot(budget_parallel(sc, j, d))) need |= 1u << j;
+        if (__ballot(!(bs.T < bs.E[j]))) spent |= 1u << j;
+    if (__ballot(par != 0u)) {  // cylinder k of budget_cyl_mask -> its slot bit
+        uint32_t c = (uint32_t)sc->budget_cyl_mask;
+#pragma unroll
+        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+            if (c) {
+                if (__ballot((par >> k) & 1u)) spent |= 1u << (__builtin_ctz(c) + 1);
+                c &= c - 1;
+            }
+        }
     }
 #pragma unroll
     for (int j = 0; j <= SR_MAX_BUDGET; j++)
-        if (!((need >> j) & 1u)) bs.E[j] = bs.E[j] - bs.T;
-    const float a = __builtin_amdgcn_sqrtf(dot(end, end));
-    for (uint32_t c = need; c; c &= c - 1) {
+        if (!((spent >> j) & 1u)) bs.E[j] = bs.E[j] - bs.T;
+    const float a = __builtin_amdgcn_sqrtf(dot(B, B));
+    uint32_t reach = 0;
+    for (uint32_t c = spent; c; c &= c - 1) {
         const int j = __builtin_ctz(c);
-        budget_set(bs, j, clearance(sc, j, end, a));
+        budget_set(bs, j, clearance(sc, j, B, a) - perr);
+        if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
     }
     bs.T = 0.0f;
     bs.m = budget_min(bs);
-    return need;
+    return reach;
 }
 
 // The test rays (frag:760-803), visited right after the black hole.
@@ -419,31 +526,24 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
     return best;
 }
 
-// intersect() for one chord of the step loop with culling: the test rays, the
-// objects tested every step (chord-culled ones only when the chord reaches
-// their bounding sphere) and the budget slots whose budget is spent. Same
+// intersect() for one exact chord of the step loop with culling: the test
+// rays, the objects tested every step (chord-culled ones only when the chord
+// reaches their bounding sphere) and the budget slots in `reach`. Same
 // winner as closest_hit_all (lexicographic keys, skipped tests provably
-// miss). One copy of each exact test: the candidates are collected into a
-// wave-uniform object mask first.
+// miss). One copy of each exact test: candidates go into a wave-uniform
+// object mask first.
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
-                                                 Budget& bs, f3 o, f3 d, float seg, f3 end) {
+                                                 uint32_t reach, f3 o, f3 d, float seg) {
     Hit best = no_hit();
     test_ray_hits(sc, segs, best, o, d, seg);
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
-    const uint32_t need = budget_step(sc, bs, d, end);
-#ifdef SR_STATS
-    for (uint32_t c = need; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
-#endif
-#ifdef SR_STATS_FIRE
-    bs.fires += (need != 0u || om != 0u) ? 1 : 0;
-#endif
-    if (need & 1u) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
+    if (reach & 1u) {  // BLACK_HOLE: sphere of radius 1 at the origin (frag:104, 757)
         f3 p;
         consider(best, sphere_test(o, d, F3(0.0f, 0.0f, 0.0f), 1.0f, seg, p), p, o, SLOT_BH, 0, KEY_BH);
     }
-    for (uint32_t c = need >> 1; c; c &= c - 1) om |= 1u << sc->budget_idx[__builtin_ctz(c)];
+    for (uint32_t c = reach >> 1; c; c &= c - 1) om |= 1u << sc->budget_idx[__builtin_ctz(c)];
     if (om) {
         const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;
         for (; om; om &= om - 1) {
@@ -455,43 +555,6 @@ __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict_
         }
     }
     return best;
-}
-
-// Upper bound of the exact chord length |ro_i - ro_(i-1)| from the orbit
-// alone (no divisions): both points are (nv cos phi + tv sin phi) / u, so
-// dv = nv (rB cB - rA cA) + tv (rB sB - rA sA) with r = 1/u approximates the
-// chord to ~1.4e-6 (rA + rB) absolute (rounding of the reference's float
-// evaluation of both points); the bound adds 8e-6 (rA + rB) and
-// a relative 1e-4 for the approximate rcp / sqrt.
-struct ChordBound {
-    f3 dv;
-    float dd, len, abs_err;
-};
-__device__ __forceinline__ ChordBound chord_bound(f3 nv, f3 tv, float rA, float rB, float cA, float sA, float cB,
-                                                  float sB) {
-    ChordBound b;
-    const float a = rB * cB - rA * cA, c = rB * sB - rA * sA;
-    b.dv = nv * a + tv * c;
-    b.dd = dot(b.dv, b.dv);
-    b.abs_err = 8.0e-6f * (rA + rB);
-    b.len = __builtin_amdgcn_sqrtf(b.dd) * 1.0001f + b.abs_err;
-    return b;
-}
-
-// Whether a budgeted cylinder may see this chord closer than SR_BUDGET_DPMIN
-// to its axis direction (then the exact chord must be tested): decided on the
-// approximate direction dv with twice the threshold, and forced when dv is
-// not known to 0.4%.
-__device__ __forceinline__ bool chord_near_parallel(const sr_dev_scene* __restrict__ sc, const ChordBound& b) {
-    const uint32_t cm = (uint32_t)sc->budget_cyl_mask;
-    if (!cm) return false;
-    bool par = !(b.abs_err <= 0.004f * __builtin_amdgcn_sqrtf(b.dd));
-    for (uint32_t c = cm; c; c &= c - 1) {
-        const sr_dev_obj& ob = sc->objs[sc->budget_idx[__builtin_ctz(c)]];
-        const float ca = dot(b.dv, ld3(ob.f + SR_F_AXES + 3));
-        par = par || !(b.dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * b.dd);
-    }
-    return par;
 }
 
 // ---- textures ------------------------------------------------
@@ -1011,16 +1074,28 @@ struct HitLog {
 // Chord end point of step j, frag:924: (nv cos phi_j + tv sin phi_j) / u_j
 __device__ __forceinline__ f3 point_at(const Ray& r, float u, float c, float s) { return (r.nv * c + r.tv * s) / u; }
 
+// The same point from an approximate radius rad ~ 1/u (no division): within
+// 1.1e-6 rad of the exact float evaluation
+__device__ __forceinline__ f3 point_near(const Ray& r, float rad, float c, float s) {
+    return r.nv * (rad * c) + r.tv * (rad * s);
+}
+
+// absolute error bound of point_near / chord components for radii rA, rB
+__device__ __forceinline__ float point_err(float rA, float rB) { return 4.0e-6f * (rA + rB); }
+
 // The step loop, frag:890-933, from step r.i (entry: r.u = u after step
 // r.i - 1, r.ro / r.rd = that step's chord end and direction).
 //
 // Lazy chords (CULL): the reference computes every chord exactly (two
 // divisions by u, a sqrt and three divisions by its length); here a step
-// whose chord provably cannot hit anything only advances (u, du) and charges
-// the clearance budgets an upper bound of its length (chord_bound). The wave
-// materialises the exact chord - the reference's float expressions on the same
-// operands, so bit-identical - when any lane's budget is spent or its chord may
-// be near-parallel to a budgeted cylinder, and at every exit and reseed.
+// only advances (u, du) and charges the clearance budgets an upper bound of
+// its chord length: with r = 1/u the chord of two orbit points is
+// sqrt((rB - rA)^2 + rA rB g) (g from the step table) up to float rounding.
+// When a budget is spent (or the chord may be near-parallel to a budgeted
+// cylinder) the wave runs a budget event on the approximate chord
+// (point_near); only when a slot may be reached is the exact chord
+// materialised - the reference's float expressions on the same operands, so
+// bit-identical - and tested. Exits and reseeds materialise it too.
 //
 // Hits that contribute vec4(0) are skipped. RECORD (sr_integrate_kernel):
 // possibly translucent hits are logged and the ray goes on; it stops at an
@@ -1032,7 +1107,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
     Budget bs;
-    if (CULL) budget_init(sc, bs, r.ro);
+    if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -1042,6 +1117,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     } out_{r, bs};
 #endif
     const int N = fr.max_steps;
+    // every chord is tested exactly when objects outside the budget slots or
+    // the test rays are present (wave-uniform)
+    const bool every = !CULL || sc->num_step > 0 || sc->tr_visible;
     // Chord bookkeeping: im = the step whose chord r.ro / r.rd hold; up = u
     // after step i - 2; (c1, s1) / (c2, s2) = cos / sin phi of steps i - 1 /
     // i - 2 (step -1: the camera, phi = 0); rA ~ 1 / u after step i - 1.
@@ -1049,7 +1127,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     float up = 0.0f;
     float c1 = 1.0f, s1 = 0.0f, c2 = 1.0f, s2 = 0.0f;
     if (r.i > 0) {
-        const float4 e1 = tbl[r.i - 1];
+        const float4 e1 = tbl[2 * r.i - 2];
         c1 = e1.z;
         s1 = e1.w;
     }
@@ -1068,10 +1146,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     };
     for (; r.i < N; r.i++) {
         const int i = r.i;
-        // {step_size, step_size / 6, cos phi, sin phi} of step i (wave-uniform)
-        const float4 e = tbl[i];
+        // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
+        const float4 e = tbl[2 * i];
+        const float g = tbl[2 * i + 1].x;
         r.steps++;
-        bool force = !CULL;
+        bool reseeded = false;
         if (r.u < fr.u_f) {  // frag:891-912
             settle_prev(i);
             f3 q;
@@ -1081,7 +1160,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
             r.u = 1.0f / len(q);
             r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-            force = true;  // new orbital frame: this chord is materialised exactly
+            if (CULL) budget_frame(sc, bs, r.nv, r.tv);
+            reseeded = true;  // new orbital frame: the chord starts at the exact r.ro
         }
         // frag:914-919
         const float h = e.x;
@@ -1106,19 +1186,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             settle_prev(i);
             return ST_BG;
         }
-        float rB = 0.0f;
-        const bool bounded = CULL && !force;  // this chord's length is charged below, else when exact
-        if (bounded) {
-            rB = __builtin_amdgcn_rcpf(un);
-            const ChordBound cb = chord_bound(r.nv, r.tv, rA, rB, c1, s1, e.z, e.w);
-            bs.T += cb.len * SR_PATH_SLACK;
-            force = !(bs.T < bs.m) || chord_near_parallel(sc, cb);
-#ifdef SR_STATS
-            SR_STAT(11, __ballot(force) && !__ballot(!(bs.T < bs.m)) ? 1 : 0);
-#endif
+        const float rB = __builtin_amdgcn_rcpf(un);
+        bool event = every || reseeded;
+        uint32_t par = 0;
+        if (CULL && !reseeded) {
+            const float dr = rB - rA;
+            const float pe = point_err(rA, rB);
+            bs.T += (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
+            par = chord_parallel(sc, bs, rB * e.z - rA * c1, rB * e.w - rA * s1, pe);
+            event = event || !(bs.T < bs.m) || par != 0u;
         }
-        SR_STAT(0, 1);
-        SR_STAT(13, __popcll(__ballot(1)));
         // advance: step i's u becomes the current one
         up = r.u;
         r.u = un;
@@ -1127,9 +1204,33 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         s2 = s1;
         c1 = e.z;
         s1 = e.w;
+        const float rAold = rA;
         rA = rB;
-        if (!__ballot(force)) continue;
-        SR_STAT(1, 1);
+        SR_STAT(0, 1);
+        SR_STAT(13, __popcll(__ballot(1)));
+        if (!__ballot(event)) continue;
+        uint32_t reach = 0xffffffffu;
+        if (CULL) {
+            // the approximate chord (exact start when materialised)
+            const bool exact_start = im == i - 1;
+            const f3 Ap = exact_start ? r.ro : point_near(r, rAold, c2, s2);
+            const f3 Bp = point_near(r, rB, e.z, e.w);
+            const float pe = point_err(exact_start ? 0.0f : rAold, rB);
+            if (reseeded) {  // chord not charged yet
+                const f3 dv = Bp - Ap;
+                bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
+                par = ~0u;  // the frame changed: the cylinders' direction test is redone exactly
+            }
+            SR_STAT(1, 1);
+            reach = budget_event(sc, bs, Ap, Bp, pe, par);
+#ifdef SR_STATS
+            for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
+#endif
+            if (!__ballot(reach != 0u || every)) continue;
+#ifdef SR_STATS_FIRE
+            bs.fires++;
+#endif
+        }
         // frag:924-930: the exact chord of step i
         f3 prev = im == i - 1 ? r.ro : point_at(r, up, c2, s2);
         r.ro = point_at(r, r.u, e.z, e.w);
@@ -1137,13 +1238,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         f3 delta = r.ro - prev;
         float seg = len(delta);
         r.rd = delta / seg;
-        rA = __builtin_amdgcn_rcpf(r.u);
-        if (CULL) {
-            if (!bounded) bs.T += seg * SR_PATH_SLACK;
-            hit = closest_hit_chord(sc, segs, bs, prev, r.rd, seg, r.ro);
-        } else {
-            hit = closest_hit_all(sc, segs, prev, r.rd, seg);
-        }
+        hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
         if (hit.slot != SLOT_NONE) {
             const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
             if (op == OP_ZERO) continue;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
@@ -1195,37 +1290,92 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #define SR_MIN_WAVES_PER_EU 5
 #endif
 
+// 1-D grid: launch slot s renders workgroup tile order[s] (costliest first,
+// sr_order_kernel), and records the tile's cost (max steps of its rays).
 template <bool CULL>
 __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
-    size_t ps_n, int* __restrict__ count) {
-    const int block = blockIdx.y * gridDim.x + blockIdx.x;
-    if (block == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+    size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
+    const int block = order ? order[blockIdx.x] : (int)blockIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+#ifdef SR_STATS
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    struct WaveLog {
+        unsigned long long t0;
+        int w;
+        __device__ ~WaveLog() {
+            if ((threadIdx.x & 63) == 0 && w < SR_WAVE_LOG) {
+                sr_wave_t[2 * w] = t0;
+                sr_wave_t[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
+    } wave_log_{t_start, block * 4 + (int)(threadIdx.x >> 6)};
+#endif
     Pix q;
-    if (!pixel_of(fr, block, threadIdx.x, q)) return;
-    const size_t id = (size_t)block * 256 + threadIdx.x;
-    Tex tx;
-    tx.bg = nullptr;
-    tx.arr = arr;
-    tx.opq = opq;
-    HitLog log{PS{ps_base, ps_n}, id, 0};
-    const PS& ps = log.ps;
-    Ray r;
-    Hit hit;
-    int st = init_pixel(fr, q, r);
-    if (st < 0) st = integrate<CULL, true>(sc, segs, tbl, fr, tx, r, hit, log);
-    ps.puti(PS_STATUS, id, st);
-    ps.puti(PS_STEPS, id, r.steps);
-    ps.puti(PS_NHITS, id, log.n);
-    ps.put3(PS_RO, id, r.ro);
-    ps.put3(PS_RD, id, r.rd);
-    if (st == ST_HIT || st == ST_MORE) {  // resumable
-        ps.puti(PS_I, id, r.i);
-        ps.put3(PS_NV, id, r.nv);
-        ps.put3(PS_TV, id, r.tv);
-        ps.at(PS_U, id) = r.u;
-        ps.at(PS_DU, id) = r.du;
+    int steps = 0;
+    if (pixel_of(fr, block, threadIdx.x, q)) {
+        const size_t id = (size_t)block * 256 + threadIdx.x;
+        Tex tx;
+        tx.bg = nullptr;
+        tx.arr = arr;
+        tx.opq = opq;
+        HitLog log{PS{ps_base, ps_n}, id, 0};
+        const PS& ps = log.ps;
+        Ray r;
+        Hit hit;
+        int st = init_pixel(fr, q, r);
+        if (st < 0) st = integrate<CULL, true>(sc, segs, tbl, fr, tx, r, hit, log);
+        ps.puti(PS_STATUS, id, st);
+        ps.puti(PS_STEPS, id, r.steps);
+        ps.puti(PS_NHITS, id, log.n);
+        ps.put3(PS_RO, id, r.ro);
+        ps.put3(PS_RD, id, r.rd);
+        if (st == ST_HIT || st == ST_MORE) {  // resumable
+            ps.puti(PS_I, id, r.i);
+            ps.put3(PS_NV, id, r.nv);
+            ps.put3(PS_TV, id, r.tv);
+            ps.at(PS_U, id) = r.u;
+            ps.at(PS_DU, id) = r.du;
+        }
+        steps = r.steps;
+    }
+    if (cost) {  // all 64 lanes are active here
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+        if ((threadIdx.x & 63) == 0) atomicMax(&cost[block], steps);
+    }
+}
+
+// Launch order for the next frame: workgroup tiles by descending cost of this
+// frame (counting sort on 256 cost buckets), so the long rays - those
+// orbiting near the photon sphere run to max_steps - start first instead of
+// forming a latency-bound tail. Resets the costs. One workgroup.
+__global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, int n, int max_cost,
+                                                        int* __restrict__ order) {
+    __shared__ int hist[256];
+    __shared__ int offs[256];
+    const int t = threadIdx.x;
+    auto bucket = [&](int c) {
+        long long b = (long long)(c < 0 ? 0 : c) * 256 / ((long long)max_cost + 1);
+        return (int)(b > 255 ? 255 : b);
+    };
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(cost[i])], 1);
+    __syncthreads();
+    if (t == 0) {
+        int run = 0;
+        for (int b = 255; b >= 0; b--) {
+            offs[b] = run;
+            run += hist[b];
+        }
+    }
+    __syncthreads();
+    for (int i = t; i < n; i += 1024) {
+        const int c = cost[i];
+        order[atomicAdd(&offs[bucket(c)], 1)] = i;
+        cost[i] = 0;
     }
 }
 
@@ -1325,34 +1475,40 @@ __global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __re
     }
 }
 
+// order/cost (optional, one int per workgroup tile): the launch order and
+// the cost feedback of sr_order_kernel
 extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
                                          const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
                                          const sr_dev_frame* fr, uint8_t* out, size_t pitch, float* dbg_rgba,
                                          int32_t* dbg_steps, float* ps, size_t ps_n, int* list, int* count,
-                                         hipEvent_t* ev4, hipStream_t stream) {
+                                         int* order, int* cost, hipEvent_t* ev4, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((fr->width + 15) / 16, (fr->nrows + 15) / 16);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
-    if ((size_t)grid.x * grid.y * 256 > ps_n) return hipErrorInvalidValue;
+    const unsigned nblocks = grid.x * grid.y;
+    if ((size_t)nblocks * 256 > ps_n) return hipErrorInvalidValue;
+    if ((order == nullptr) != (cost == nullptr)) return hipErrorInvalidValue;
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (cull)
-        hipLaunchKernelGGL(sr_integrate_kernel<true>, grid, block, 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n,
-                           count);
+        hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(nblocks), block, 0, stream, sc, tbl, segs, arr, opq, *fr,
+                           ps, ps_n, count, order, cost);
     else
-        hipLaunchKernelGGL(sr_integrate_kernel<false>, grid, block, 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n,
-                           count);
+        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(nblocks), block, 0, stream, sc, tbl, segs, arr, opq, *fr,
+                           ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
     hipLaunchKernelGGL(sr_shade_kernel, grid, block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n, out, pitch, dbg_rgba,
                        dbg_steps, list, count);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
-    unsigned nb = grid.x * grid.y < 1024u ? grid.x * grid.y : 1024u;
+    unsigned nb = nblocks < 1024u ? nblocks : 1024u;
     if (cull)
         hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     else
         hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
+    if (order)
+        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(1024), 0, stream, cost, (int)nblocks, fr->max_steps, order);
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }
@@ -1364,6 +1520,14 @@ extern "C" int sr_debug_stats(unsigned long long* out32) {
     if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
     unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z) != hipSuccess) return -3;
+    return 0;
+}
+extern "C" int sr_debug_wave_times(unsigned long long* out, int n_waves) {
+    if (n_waves < 0 || n_waves > SR_WAVE_LOG) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_wave_t), 2 * (size_t)n_waves * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -3;
     return 0;
 }
 #endif

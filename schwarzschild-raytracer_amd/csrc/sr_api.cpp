@@ -5,6 +5,7 @@
 // become sr_set_scene / sr_set_test_ray snapshots.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -20,8 +21,8 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                                          const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
                                          const sr_dev_frame* fr,
                                          uint8_t* out, size_t pitch, float* dbg_rgba, int32_t* dbg_steps,
-                                         float* ps, size_t ps_n, int* list, int* count, hipEvent_t* ev4,
-                                         hipStream_t stream);
+                                         float* ps, size_t ps_n, int* list, int* count, int* order, int* cost,
+                                         hipEvent_t* ev4, hipStream_t stream);
 
 namespace {
 
@@ -53,6 +54,11 @@ struct sr_ctx {
     int* d_list = nullptr;
     int* d_count = nullptr;
     size_t ps_n = 0;
+    // workgroup-tile launch order (costliest first) and per-tile cost of the
+    // last frame on this grid shape (geodesic.hip sr_order_kernel)
+    int* d_order = nullptr;
+    int* d_cost = nullptr;
+    int order_gx = 0, order_gy = 0;
     // optional per-kernel timing: 4 events per frame (before integrate, after
     // integrate, after shade, after resume), a ring of `timing_cap` frames
     std::vector<hipEvent_t> tev;
@@ -103,12 +109,16 @@ void set_bound(sr_dev_obj& o, V3 c, float R, int kind, float mu) {
     o.rb = R + SR_MU_QUADRATIC * (1.f + l1norm(c) + R);
     o.mu = mu;
     o.kind = kind;
-    // plane clearance (disk, hollow disk, rectangle): the plane through f[pos]
-    // with normal axes[1] must be a unit normal for |n.(A - pos)| to be a distance
+    // distance-to-primitive clearance (kernel clearance()): disks need a unit
+    // normal axes[1]; rectangles, boxes and cylinders are only budgeted with an
+    // orthonormal frame. Margin for the primitives' in-plane / height / radius
+    // tests, relative to their magnitudes.
     V3 n = ld(o.f + SR_F_AXES + 3);
-    bool planar = o.type == SR_OBJECT_DISK || o.type == SR_OBJECT_HOLLOW_DISK || o.type == SR_OBJECT_RECTANGLE;
-    o.mp = planar && std::fabs(dot(n, n) - 1.f) < 1e-5f ? SR_MU_QUADRATIC * (1.f + l1norm(ld(o.f + SR_F_POS)))
-                                                         : INFINITY;
+    bool typed = o.type == SR_OBJECT_DISK || o.type == SR_OBJECT_HOLLOW_DISK || o.type == SR_OBJECT_RECTANGLE ||
+                 o.type == SR_OBJECT_BOX || o.type == SR_OBJECT_CYLINDER;
+    o.mp = typed && std::fabs(dot(n, n) - 1.f) < 1e-5f
+               ? SR_MU_QUADRATIC * (1.f + l1norm(ld(o.f + SR_F_POS)) + R)
+               : INFINITY;
     o.pl1 = l1norm(ld(o.f + SR_F_POS));
 }
 
@@ -163,7 +173,7 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
                 o.br = INFINITY;
                 o.rb = INFINITY;
                 o.mu = SR_MU_PLANAR;
-                o.mp = SR_MU_QUADRATIC * (1.f + l1norm(pos));
+                o.mp = SR_MU_QUADRATIC * (1.f + l1norm(pos));  // plane distance only
                 o.pl1 = l1norm(pos);
                 o.kind = SR_KIND_BUDGET;
             }
@@ -267,14 +277,26 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
     }
     // frag:860, 914-915, 925: the angle sequence depends only on the step index
     const float max_angle = 2.0f * (float)max_revs * kPi;
-    // entry i = {step_size, step_size / 6, cos phi, sin phi}; one padding entry
-    // so the kernel can prefetch i + 1 unconditionally
-    std::vector<float4> h((size_t)max_steps + 1, make_float4(0.f, 0.f, 0.f, 0.f));
+    // entry i = two float4: {step_size, step_size / 6, cos phi, sin phi} and
+    // {g, 0, 0, 0} with g = 2 (sqrt(n_(i-1) n_i) - p_i) for the float unit
+    // vectors (cos, sin) of steps i - 1 and i (n = squared norm, p = their dot;
+    // step -1 is phi = 0): the squared chord of two orbit points at radii
+    // r1, r2 is (r2 - r1)^2 + r1 r2 g up to float rounding (kernel chord
+    // bound). One padding entry.
+    std::vector<float4> h(2 * ((size_t)max_steps + 1), make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
+    double c1 = 1.0, s1 = 0.0;
     for (int i = 0; i < max_steps; i++) {
         float step = (max_angle - phi) / (float)(max_steps - i);
         phi += step;
-        h[i] = make_float4(step, step / 6.0f, (float)std::cos((double)phi), (float)std::sin((double)phi));
+        const float c = (float)std::cos((double)phi), sn = (float)std::sin((double)phi);
+        h[2 * (size_t)i] = make_float4(step, step / 6.0f, c, sn);
+        const double n1 = c1 * c1 + s1 * s1, n2 = (double)c * c + (double)sn * sn, pr = c1 * c + s1 * sn;
+        double g = 2.0 * (std::sqrt(n1 * n2) - pr);
+        g = g > 0.0 ? g * (1.0 + 1e-6) + 1e-30 : 1e-30;  // rounded up
+        h[2 * (size_t)i + 1] = make_float4((float)g, 0.f, 0.f, 0.f);
+        c1 = c;
+        s1 = sn;
     }
     Table t;
     t.steps = max_steps;
@@ -367,6 +389,37 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
     return SR_OK;
 }
 
+// Launch order for a new grid shape: tiles nearest the frame centre first
+// (where the black hole usually is) until a frame has measured the costs.
+int ensure_order(sr_ctx* ctx, int gx, int gy) {
+    if (ctx->order_gx == gx && ctx->order_gy == gy && ctx->d_order) return SR_OK;
+    if (ctx->order_gx || ctx->order_gy) {
+        if (!hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    }
+    if (ctx->d_order) (void)hipFree(ctx->d_order);
+    if (ctx->d_cost) (void)hipFree(ctx->d_cost);
+    ctx->d_order = nullptr;
+    ctx->d_cost = nullptr;
+    ctx->order_gx = ctx->order_gy = 0;
+    const size_t n = (size_t)gx * gy;
+    std::vector<int> ord(n);
+    std::vector<double> d(n);
+    for (size_t i = 0; i < n; i++) {
+        ord[i] = (int)i;
+        const double x = (double)(i % gx) + 0.5 - 0.5 * gx, y = (double)(i / gx) + 0.5 - 0.5 * gy;
+        d[i] = x * x + y * y;
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return d[a] < d[b]; });
+    if (!hip_ok(hipMalloc(&ctx->d_order, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_cost, n * sizeof(int))))
+        return SR_E_NOMEM;
+    if (!hip_ok(hipMemcpy(ctx->d_order, ord.data(), n * sizeof(int), hipMemcpyHostToDevice)) ||
+        !hip_ok(hipMemset(ctx->d_cost, 0, n * sizeof(int))))
+        return SR_E_HIP;
+    ctx->order_gx = gx;
+    ctx->order_gy = gy;
+    return SR_OK;
+}
+
 int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
     if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
     if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
@@ -419,8 +472,13 @@ int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width
     if (rc != SR_OK) return rc;
     rc = ensure_pixel_state(ctx, (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) * 256);
     if (rc != SR_OK) return rc;
+    if (nrows > 0) {
+        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16);
+        if (rc != SR_OK) return rc;
+    }
     hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
                                       dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count,
+                                      nrows > 0 ? ctx->d_order : nullptr, nrows > 0 ? ctx->d_cost : nullptr,
                                       ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
                                       reinterpret_cast<hipStream_t>(stream));
     return hip_ok(e) ? SR_OK : SR_E_HIP;
@@ -488,6 +546,8 @@ void sr_destroy(sr_ctx* c) {
     if (c->d_opq) (void)hipFree(c->d_opq);
     for (auto& kv : c->tables) (void)hipFree(kv.second.dev);
     free_pixel_state(c);
+    if (c->d_order) (void)hipFree(c->d_order);
+    if (c->d_cost) (void)hipFree(c->d_cost);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     delete c;
 }

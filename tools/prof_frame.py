@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--no-cull", action="store_true")
+    ap.add_argument("--scene", default="tex", choices=["tex", "untex", "bh"])
     args = ap.parse_args()
     import torch
 
@@ -24,7 +25,10 @@ def main():
     pkg = srpkg.load_package()
     abi, sc = pkg.abi, pkg.scenes
     r = pkg.Renderer(0)
-    r.set_scene(sc.scene_default(textured=True))
+    if args.scene == "bh":
+        r.set_scene(sc.scene_black_hole_only())
+    else:
+        r.set_scene(sc.scene_default(textured=args.scene == "tex"))
     r.set_background(sc.skybox(2048, 1024))
     arr, _, _ = sc.default_texture_array()
     r.set_texture_array(arr)

@@ -47,7 +47,28 @@ def main():
     assert lib.sr_debug_stats(buf) == 0
     out = {NAMES.get(k, f"slot{k - 2}_tested" if 2 <= k <= 10 else str(k)): int(buf[k]) for k in range(14)}
     out["fired_frac"] = out["fired"] / max(1, out["wave_steps"])
-    print(json.dumps(out, indent=1))
+    # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
+    import numpy as np
+
+    nw = ((1920 + 15) // 16) * ((1080 + 15) // 16) * 4
+    tb = (C.c_ulonglong * (2 * nw))()
+    lib.sr_debug_wave_times.restype = C.c_int
+    lib.sr_debug_wave_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    assert lib.sr_debug_wave_times(tb, nw) == 0
+    t = np.frombuffer(tb, dtype=np.uint64).reshape(nw, 2).astype(np.int64)
+    t = t[t[:, 1] > 0]
+    t0 = t[:, 0].min()
+    s_, e_ = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0  # microseconds
+    span = e_.max()
+    grid = np.linspace(0, span, 41)
+    active = [int(((s_ <= x) & (e_ > x)).sum()) for x in grid]
+    out["timeline_us"] = round(float(span), 1)
+    out["active_waves_at_5pct"] = active
+    out["wave_us_mean"] = round(float((e_ - s_).mean()), 1)
+    out["wave_us_max"] = round(float((e_ - s_).max()), 1)
+    out["last_start_us"] = round(float(s_.max()), 1)
+    out["busy_frac"] = round(float((e_ - s_).sum() / (span * max(active))), 3)
+    print(json.dumps(out))
     r.close()
 
 
