@@ -99,6 +99,111 @@ def scene_black_hole_only() -> abi.Scene:
     return s
 
 
+def _rand_axes(rng, skew: bool) -> list[float]:
+    """Column-major axes of a random rotation (optionally one column scaled:
+    a non-orthonormal frame the culling must treat as unbounded)."""
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    m = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                  [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                  [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+    if skew:
+        m[:, rng.integers(0, 3)] *= 1.3
+    return [float(np.float32(v)) for v in m.T.reshape(-1)]
+
+
+def scene_random(seed: int, n_objects: int = 21, translucent: bool = True, planes: bool = True) -> abi.Scene:
+    """A stress scene: up to 3 of every primitive type (21 objects: more than
+    the kernel's budget slots), random poses at r in [2.5, 25], some skewed
+    frames, random materials (textures, normal maps, single-sided faces,
+    flipped normals, alpha < 1) and 1-4 lights."""
+    rng = np.random.default_rng(seed)
+    s = abi.Scene()
+    abi.load().sr_scene_clear(C.byref(s))
+    set_scene_texture_sizes(s, [(600, 600), (1601, 1201)], (1601, 1201))
+    for m in range(abi.MAX_MATERIALS):
+        mat = s.materials[m]
+        for k in range(3):
+            mat.color[k] = float(np.float32(rng.uniform(0.1, 1.0)))
+        mat.color[3] = 1.0 if (not translucent or rng.uniform() < 0.6) else float(np.float32(rng.choice([0.0, 0.5])))
+        mat.ambient = float(np.float32(rng.uniform(0.0, 0.3)))
+        mat.diffuse = float(np.float32(rng.uniform(0.3, 1.0)))
+        mat.specular = float(np.float32(rng.uniform(0.0, 1.0)))
+        mat.shininess = float(np.float32(rng.choice([4.0, 32.0, 100.0])))
+        mat.texture_index = int(rng.choice([-1, 0, 1]))
+        mat.normal_map_index = int(rng.choice([-1, -1, -1, 0]))
+        mat.invert_uv_x = int(rng.uniform() < 0.2)
+        mat.invert_uv_y = int(rng.uniform() < 0.2)
+        mat.swap_uvs = int(rng.uniform() < 0.2)
+        mat.double_sided_normals = int(rng.uniform() < 0.5)
+        mat.flip_normals = int(rng.uniform() < 0.2)
+    s.num_lights = int(rng.integers(1, abi.MAX_LIGHTS + 1))
+    for i in range(s.num_lights):
+        L = s.lights[i]
+        for k in range(3):
+            L.transform.pos[k] = float(np.float32(rng.uniform(-15, 15)))
+            L.color[k] = float(np.float32(rng.uniform(0.5, 1.0)))
+        L.intensity = float(np.float32(rng.uniform(2, 10)))
+        L.attenuation_constant, L.attenuation_linear, L.attenuation_quadratic = 1.0, 0.09, 0.032
+    types = [t for t in range(7) for _ in range(3) if planes or t != abi.OBJECT_PLANE]
+    rng.shuffle(types)
+    counts = [0] * 7
+    n = 0
+    for t in types[:n_objects]:
+        k = counts[t]
+        counts[t] += 1
+        v = rng.normal(size=3)
+        v = v / np.linalg.norm(v) * rng.uniform(2.5, 25.0)
+        skew = t in (abi.OBJECT_CYLINDER, abi.OBJECT_RECTANGLE, abi.OBJECT_BOX) and rng.uniform() < 0.2
+        tr = abi.Transform()
+        for i in range(3):
+            tr.pos[i] = float(np.float32(v[i]))
+        ax = _rand_axes(rng, skew)
+        for i in range(9):
+            tr.axes[i] = ax[i]
+
+        def plane(p):
+            p.transform = tr
+            p.texture_offset[0] = float(np.float32(rng.uniform(-1, 1)))
+            p.texture_offset[1] = float(np.float32(rng.uniform(-1, 1)))
+            p.repeat_texture = int(rng.uniform() < 0.5)
+            p.texture_size[0] = float(np.float32(rng.uniform(1, 4)))
+            p.texture_size[1] = float(np.float32(rng.uniform(1, 4)))
+
+        if t == abi.OBJECT_SPHERE:
+            s.spheres[k].transform = tr
+            s.spheres[k].radius = float(np.float32(rng.uniform(0.3, 2.5)))
+        elif t == abi.OBJECT_PLANE:
+            plane(s.planes[k])
+        elif t == abi.OBJECT_DISK:
+            plane(s.disks[k].plane)
+            s.disks[k].radius = float(np.float32(rng.uniform(0.5, 3.0)))
+        elif t == abi.OBJECT_HOLLOW_DISK:
+            plane(s.hollow_disks[k].plane)
+            r0 = rng.uniform(0.5, 3.0)
+            s.hollow_disks[k].inner_radius = float(np.float32(r0))
+            s.hollow_disks[k].outer_radius = float(np.float32(r0 + rng.uniform(0.5, 3.0)))
+        elif t == abi.OBJECT_CYLINDER:
+            s.cylinders[k].transform = tr
+            s.cylinders[k].height = float(np.float32(rng.uniform(0.5, 5.0)))
+            s.cylinders[k].radius = float(np.float32(rng.uniform(0.2, 2.0)))
+        elif t == abi.OBJECT_RECTANGLE:
+            plane(s.rectangles[k].plane)
+            s.rectangles[k].width = float(np.float32(rng.uniform(0.5, 4.0)))
+            s.rectangles[k].height = float(np.float32(rng.uniform(0.5, 4.0)))
+        else:
+            s.boxes[k].transform = tr
+            s.boxes[k].width = float(np.float32(rng.uniform(0.3, 2.0)))
+            s.boxes[k].depth = float(np.float32(rng.uniform(0.3, 2.0)))
+            s.boxes[k].height = float(np.float32(rng.uniform(0.3, 2.0)))
+        o = s.objects[n]
+        o.type, o.index, o.material_index = t, k, int(rng.integers(0, abi.MAX_MATERIALS))
+        n += 1
+    s.num_objects = n
+    return s
+
+
 def set_scene_texture_sizes(s: abi.Scene, sizes, max_size) -> None:
     for i, (w, h) in enumerate(sizes):
         s.texture_sizes[i][0] = float(w)

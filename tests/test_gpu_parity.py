@@ -208,3 +208,65 @@ def test_headline_frame_sampled_rows(pkg, gpu, oracle, oracle_tex):
         assert (rs[0] != s[y]).mean() <= 1e-3, f"row {y}"
     # mean executed steps per pixel at N=2000 ~ 0.206 N
     assert 380 < s.mean() < 440, s.mean()
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_scenes(pkg, gpu, oracle, oracle_tex, seed):
+    """Stress scenes: 18-21 objects - more than the
+    kernel's budget slots, so some are tested per chord - skewed frames
+    (unbounded for culling), translucent and single-sided materials (logged
+    hits, resumed rays), normal maps, planes in every other scene."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_random(seed, planes=seed % 2 == 0)
+    cam = sc.random_camera(300 + seed)
+    params = abi.default_params(max_steps=600, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, cam, params, 96, 54)
+    o = oracle.render(scene, cam, params, 96, 54, oracle_tex)
+    compare(g, o, f"random scene {seed}")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_scenes_culling_exact(pkg, gpu, seed):
+    """Culling, lazy chords and hit classification must not change a bit on
+    the stress scenes either."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    gpu.set_scene(sc.scene_random(100 + seed, planes=seed % 2 == 1))
+    gpu.set_test_ray(abi.default_test_ray())
+    cam = sc.random_camera(400 + seed)
+    params = abi.default_params(max_steps=1500, percent_black=-1.0)
+    outs = []
+    for cull in (True, False):
+        gpu.set_culling(cull)
+        f, b, s = gpu.render_debug(cam, params, 320, 180)
+        torch.cuda.synchronize()
+        outs.append((f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()))
+    gpu.set_culling(True)
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+
+
+def test_test_ray_far_view(pkg, gpu, oracle, oracle_tex):
+    """A visible press-R polyline seen from far away: every chord must be
+    tested against the test-ray cylinders even where no budget is spent."""
+    sc, abi = pkg.scenes, pkg.abi
+    cam0 = sc.camera_look((4.0, 1.0, 12.0), (-0.3, -0.05, -1.0))
+    fwd = list(cam0.transform.axes[6:9])
+    pts = abi.test_ray_points(list(cam0.transform.pos), fwd, 300, 2)
+    tr = abi.default_test_ray()
+    tr.visible = 1
+    tr.num_curved_points = len(pts)
+    for i, p in enumerate(pts):
+        tr.curved_points[i][0], tr.curved_points[i][1], tr.curved_points[i][2] = p
+    for k in range(3):
+        tr.flat_origin[k] = cam0.transform.pos[k] + fwd[k]
+        tr.flat_dir[k] = fwd[k]
+    view = sc.camera_look((0.0, 25.0, 45.0), (0.0, -25.0, -45.0), fov=60.0)
+    scene = sc.scene_black_hole_only()
+    params = abi.default_params(max_steps=800, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, view, params, 96, 54, tr)
+    o = oracle.render(scene, view, params, 96, 54, oracle_tex, tr)
+    compare(g, o, "test ray far view")
+    assert (g[0][..., :3] != o[0][..., :3]).sum() == 0
+    gpu.set_test_ray(abi.default_test_ray())
