@@ -6,7 +6,7 @@
  *
  *   reference                                              replaced by
  *   -----------------------------------------------------  -------------------------
- *   glDrawElements(full-screen quad)  src/main.cpp:318-319  sr_render / sr_render_rows
+ *   glDrawElements(full-screen quad)  src/main.cpp:318-319  sr_render / sr_render_blocks
  *   Camera::loadShader                camera.cpp:41-50      sr_camera argument
  *   ObjectLoader::load                objectLoader.cpp:27   sr_set_scene (snapshot)
  *   loadTexture(bg) + unit 0          image_utils.cpp:7-40  sr_set_background
@@ -260,7 +260,10 @@ int sr_set_test_ray(sr_ctx* ctx, const sr_test_ray* test_ray);
 
 /* Render rows [row_begin, row_end) of a width x height frame (GL order: row 0
  * is the bottom row) into dev_rgba8 (device memory, row r at
- * dev_rgba8 + (r - row_begin) * pitch_bytes). Asynchronous on `stream`. */
+ * dev_rgba8 + (r - row_begin) * pitch_bytes). Asynchronous on `stream`.
+ * A context reuses its per-frame scratch (pixel state, launch order), so its
+ * renders must be ordered: one stream per context, or synchronise between
+ * streams. */
 int sr_render(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width,
               int height, int row_begin, int row_end, uint8_t* dev_rgba8,
               size_t pitch_bytes, sr_stream stream);

@@ -954,7 +954,7 @@ __device__ __forceinline__ uint32_t unorm8(float x) {
 }
 
 // ---- pixel pipeline ---------------------------------------------------------
-// A frame is three launches on one stream (DESIGN.md §3):
+// A frame is three launches on one stream (DESIGN.md §6):
 //   sr_integrate_kernel : camera ray + RK4 step loop (integration registers
 //                         only). Chord hits are classified by hit_opacity:
 //                         back faces are skipped, hits that may be translucent
