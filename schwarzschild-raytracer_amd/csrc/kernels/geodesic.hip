@@ -81,12 +81,13 @@ struct Tex {
 
 #ifdef SR_STATS
 // Measurement builds only: wave-level event counters (tools/stats_frame.py).
-//   0 wave-steps  1 fired wave-steps  2..10 slot j tested  11 fired by the
-//   parallel / forced rule only  12 exact object tests run  13 lane-steps
+//   0 wave-steps  1 budget events  2..10 slot j reached (exact chord)
+//   11 -  12 exact object tests run  13 lane-steps  14..22 slot j spent
 __device__ unsigned long long sr_stats[32];
 // per-wave [start, end] s_memrealtime (100 MHz) of sr_integrate_kernel, by wave index
 #define SR_WAVE_LOG (1 << 17)
-__device__ unsigned long long sr_wave_t[2 * SR_WAVE_LOG];
+#define SR_WAVE_REC 16  // t0, t1, max steps, events << 32 | exact chords, reach count of slots 0..8
+__device__ unsigned long long sr_wave_t[SR_WAVE_REC * SR_WAVE_LOG];
 __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
     const unsigned long long act = __ballot(1);
     if ((int)__lane_id() == __builtin_ctzll(act)) atomicAdd(&sr_stats[k], v);
@@ -302,7 +303,9 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
     float c;
     if (j == 0) {
-        c = a - (1.0f + SR_MU_QUADRATIC * 3.0f);  // black hole: centre 0, R = 1
+        // black hole: sphere_test accepts only its entry or exit point, on the
+        // r = 1 shell (a ray can cross the shell between steps and go on inside)
+        c = fabsf(a - 1.0f) - SR_MU_QUADRATIC * 3.0f;
     } else {
         const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
         f3 w = A - ld3(ob.bc);
@@ -433,15 +436,55 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
     const float dd = dot(dv, dv);
     const float len = __builtin_amdgcn_sqrtf(dd);
     const float S = ((fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + len + 1.0f) * 1.001f + perr;
+    if (!(S < 1.0e30f)) return true;  // non-finite chord: the exact tests decide
     f3 c;
     float R;
     if (j == 0) {
         c = F3(0.0f, 0.0f, 0.0f);
         R = 1.0f + SR_MU_QUADRATIC * S;  // the black hole: sphere r = 1 at the origin
+        // a chord inside the shell (both ends, by the margin) cannot reach it
+        const float ri = (1.0f - SR_MU_QUADRATIC * S) * 0.999f - perr;
+        if (dot(A, A) < ri * ri && dot(B, B) < ri * ri && ri > 0.0f) return false;
     } else {
         const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
         c = ld3(ob.bc);
         R = ob.br + ob.mu * S;
+        if (ob.mp < INFINITY) {  // orthonormal frame: tighter regions than the bounding sphere
+            const float m = (ob.mp + SR_MU_QUADRATIC * S) * 1.001f + perr;
+            const f3 pos = ld3(ob.f + SR_F_POS);
+            const f3 a1 = ld3(ob.f + SR_F_AXES + 3);
+            const float yA = dot(A - pos, a1), yB = dot(B - pos, a1);
+            if (ob.type == SR_OBJECT_PLANE || ob.type == SR_OBJECT_DISK || ob.type == SR_OBJECT_HOLLOW_DISK ||
+                ob.type == SR_OBJECT_RECTANGLE) {
+                // planar: the chord must reach the plane's acceptance slab
+                if ((yA > m && yB > m) || (yA < -m && yB < -m)) return false;
+            } else if (ob.type == SR_OBJECT_BOX) {
+                // the chord must reach the box grown by the margin (slab test in the box frame)
+                const f3 a0 = ld3(ob.f + SR_F_AXES), a2 = ld3(ob.f + SR_F_AXES + 6);
+                const float xA = dot(A - pos, a0), xB = dot(B - pos, a0);
+                const float zA = dot(A - pos, a2), zB = dot(B - pos, a2);
+                float t0 = 0.0f, t1 = 1.0f;
+                auto slab = [&](float pA, float pB, float hi) {
+                    const float lo_ = -m, hi_ = hi + m, dpv = pB - pA;
+                    if (fabsf(dpv) < 1e-30f) {
+                        if (pA < lo_ || pA > hi_) t1 = -1.0f;
+                        return;
+                    }
+                    float ta = (lo_ - pA) / dpv, tb = (hi_ - pA) / dpv;
+                    if (ta > tb) {
+                        const float tt = ta;
+                        ta = tb;
+                        tb = tt;
+                    }
+                    t0 = fmaxf(t0, ta);
+                    t1 = fminf(t1, tb);
+                };
+                slab(xA, xB, ob.f[12]);
+                slab(yA, yB, ob.f[14]);
+                slab(zA, zB, ob.f[13]);
+                if (t0 > t1 + 1e-6f) return false;
+            }
+        }
         if (ob.type == SR_OBJECT_CYLINDER) {
             const float ca = dot(dv, ld3(ob.f + SR_F_AXES + 3));
             const float dp = (dd - ca * ca) * __builtin_amdgcn_rcpf(dd) * 0.5f;
@@ -486,6 +529,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         if (!((spent >> j) & 1u)) bs.E[j] = bs.E[j] - bs.T;
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
+#ifdef SR_STATS
+    for (uint32_t c = spent; c; c &= c - 1) SR_STAT(14 + __builtin_ctz(c), 1);
+#endif
     for (uint32_t c = spent; c; c &= c - 1) {
         const int j = __builtin_ctz(c);
         budget_set(bs, j, clearance(sc, j, B, a) - perr);
@@ -984,6 +1030,10 @@ struct Ray {
     f3 ro, rd, nv, tv;
     float u, du;
     int i, steps;
+#ifdef SR_STATS
+    int ev, mat;  // budget events, exact chords (measurement builds)
+    int rc[SR_MAX_BUDGET + 1];
+#endif
 };
 
 struct Pix {
@@ -1049,6 +1099,11 @@ __device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const Pix& q, 
     r.nv = nrm(r.ro);
     r.steps = 0;
     r.i = 0;
+#ifdef SR_STATS
+    r.ev = 0;
+    r.mat = 0;
+    for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] = 0;
+#endif
     const bool flat = fr.raytrace_type == SR_RAYTRACE_FLAT ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_WIDTH && uv.x > 2.0f * fr.curved_percentage + -1.0f) ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_HEIGHT && uv.y > 2.0f * fr.curved_percentage + -1.0f);
@@ -1222,9 +1277,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 par = ~0u;  // the frame changed: the cylinders' direction test is redone exactly
             }
             SR_STAT(1, 1);
+#ifdef SR_STATS
+            r.ev++;
+#endif
             reach = budget_event(sc, bs, Ap, Bp, pe, par);
 #ifdef SR_STATS
             for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
+#pragma unroll
+            for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] += (reach >> j) & 1u;
 #endif
             if (!__ballot(reach != 0u || every)) continue;
 #ifdef SR_STATS_FIRE
@@ -1232,6 +1292,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
         }
         // frag:924-930: the exact chord of step i
+#ifdef SR_STATS
+        r.mat++;
+#endif
         f3 prev = im == i - 1 ? r.ro : point_at(r, up, c2, s2);
         r.ro = point_at(r, r.u, e.z, e.w);
         im = i;
@@ -1299,18 +1362,18 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
     const int block = order ? order[blockIdx.x] : (int)blockIdx.x;
     if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+#ifndef SR_PRIO_BLOCKS
+#define SR_PRIO_BLOCKS 256
+#endif
+    // The costliest tiles (launched first) are the frame's critical path: a
+    // 2000-step ray sharing its SIMD with four other waves would run 3x longer
+    // than the rest of the grid. Raised issue priority keeps them near their
+    // own latency bound while the other waves fill the idle issue slots.
+    if (order && blockIdx.x < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
 #ifdef SR_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    struct WaveLog {
-        unsigned long long t0;
-        int w;
-        __device__ ~WaveLog() {
-            if ((threadIdx.x & 63) == 0 && w < SR_WAVE_LOG) {
-                sr_wave_t[2 * w] = t0;
-                sr_wave_t[2 * w + 1] = __builtin_amdgcn_s_memrealtime();
-            }
-        }
-    } wave_log_{t_start, block * 4 + (int)(threadIdx.x >> 6)};
+    unsigned long long evmat = 0;
+    int rcv[SR_MAX_BUDGET + 1] = {};
 #endif
     Pix q;
     int steps = 0;
@@ -1339,7 +1402,36 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
             ps.at(PS_DU, id) = r.du;
         }
         steps = r.steps;
+#ifdef SR_STATS
+        evmat = ((unsigned long long)r.ev << 32) | (unsigned)r.mat;
+        for (int j = 0; j <= SR_MAX_BUDGET; j++) rcv[j] = r.rc[j];
+#endif
     }
+#ifdef SR_STATS
+    {
+        int sm = steps;
+        unsigned long long em = evmat;
+        for (int off = 32; off > 0; off >>= 1) {
+            sm = max(sm, __shfl_xor(sm, off));
+            const unsigned long long o = __shfl_xor(em, off);
+            em = o > em ? o : em;
+        }
+        int rcm[SR_MAX_BUDGET + 1];
+        for (int j = 0; j <= SR_MAX_BUDGET; j++) {
+            rcm[j] = rcv[j];
+            for (int off = 32; off > 0; off >>= 1) rcm[j] = max(rcm[j], __shfl_xor(rcm[j], off));
+        }
+        const int w = block * 4 + (int)(threadIdx.x >> 6);
+        if ((threadIdx.x & 63) == 0 && w < SR_WAVE_LOG) {
+            unsigned long long* rec = sr_wave_t + (size_t)SR_WAVE_REC * w;
+            rec[0] = t_start;
+            rec[1] = __builtin_amdgcn_s_memrealtime();
+            rec[2] = (unsigned long long)sm;
+            rec[3] = em;
+            for (int j = 0; j <= SR_MAX_BUDGET; j++) rec[4 + j] = (unsigned long long)rcm[j];
+        }
+    }
+#endif
     if (cost) {  // all 64 lanes are active here
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
@@ -1525,7 +1617,7 @@ extern "C" int sr_debug_stats(unsigned long long* out32) {
 extern "C" int sr_debug_wave_times(unsigned long long* out, int n_waves) {
     if (n_waves < 0 || n_waves > SR_WAVE_LOG) return -1;
     if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_wave_t), 2 * (size_t)n_waves * sizeof(unsigned long long)) !=
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_wave_t), SR_WAVE_REC * (size_t)n_waves * sizeof(unsigned long long)) !=
         hipSuccess)
         return -3;
     return 0;

@@ -12,7 +12,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-NAMES = {0: "wave_steps", 1: "fired", 11: "fired_parallel_only", 12: "object_tests", 13: "lane_steps"}
+NAMES = {0: "wave_steps", 1: "events", 11: "unused", 12: "object_tests", 13: "lane_steps"}
 
 
 def main():
@@ -43,19 +43,27 @@ def main():
     params = abi.default_params(max_steps=args.max_steps, percent_black=-1.0)
     buf = (C.c_ulonglong * 32)()
     lib.sr_debug_stats(buf)  # clear
-    r.render(cam, params, 1920, 1080)
+    r.render(cam, params, 1920, 1080)  # first frame: centre-out launch order
+    lib.sr_debug_stats(buf)  # clear
+    r.render(cam, params, 1920, 1080)  # steady state: cost-ordered launch
     assert lib.sr_debug_stats(buf) == 0
-    out = {NAMES.get(k, f"slot{k - 2}_tested" if 2 <= k <= 10 else str(k)): int(buf[k]) for k in range(14)}
-    out["fired_frac"] = out["fired"] / max(1, out["wave_steps"])
+    def name(k):
+        if k in NAMES:
+            return NAMES[k]
+        return f"slot{k - 2}_reached" if 2 <= k <= 10 else f"slot{k - 14}_spent"
+
+    out = {name(k): int(buf[k]) for k in range(23)}
+    out["event_frac"] = out["events"] / max(1, out["wave_steps"])
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
 
     nw = ((1920 + 15) // 16) * ((1080 + 15) // 16) * 4
-    tb = (C.c_ulonglong * (2 * nw))()
+    tb = (C.c_ulonglong * (16 * nw))()
     lib.sr_debug_wave_times.restype = C.c_int
     lib.sr_debug_wave_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     assert lib.sr_debug_wave_times(tb, nw) == 0
-    t = np.frombuffer(tb, dtype=np.uint64).reshape(nw, 2).astype(np.int64)
+    t = np.frombuffer(tb, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
+    wid = np.arange(nw)[t[:, 1] > 0]
     t = t[t[:, 1] > 0]
     t0 = t[:, 0].min()
     s_, e_ = (t[:, 0] - t0) / 100.0, (t[:, 1] - t0) / 100.0  # microseconds
@@ -68,6 +76,17 @@ def main():
     out["wave_us_max"] = round(float((e_ - s_).max()), 1)
     out["last_start_us"] = round(float(s_.max()), 1)
     out["busy_frac"] = round(float((e_ - s_).sum() / (span * max(active))), 3)
+    dur = e_ - s_
+    top = np.argsort(-dur)[:8]
+    gx = (1920 + 15) // 16
+    out["slowest_waves"] = [
+        {"us": round(float(dur[k]), 1), "start_us": round(float(s_[k]), 1), "block_xy": [int(wid[k] // 4 % gx), int(wid[k] // 4 // gx)],
+         "wave": int(wid[k] % 4), "max_steps": int(t[k, 2]), "events": int(t[k, 3] >> 32), "exact_chords": int(t[k, 3] & 0xffffffff),
+         "reach_by_slot": [int(x) for x in t[k, 4:13]]}
+        for k in top]
+    ms = t[:, 2].astype(float)
+    out["us_per_step_by_steps"] = {f"{lo}-{hi}": round(float((dur[(ms >= lo) & (ms < hi)] / ms[(ms >= lo) & (ms < hi)]).mean()), 3)
+                                   for lo, hi in [(100, 500), (500, 1000), (1000, 1500), (1500, 2001)] if ((ms >= lo) & (ms < hi)).any()}
     print(json.dumps(out))
     r.close()
 
