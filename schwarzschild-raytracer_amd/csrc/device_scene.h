@@ -52,8 +52,12 @@
 // Budgeted cylinders: chords with |d_perp|^2 < SR_BUDGET_DPMIN are tested per
 // chord; the budget window is capped at SR_BUDGET_TMAX of path so the
 // quadratic margin can be bounded at the anchor.
+#ifndef SR_BUDGET_DPMIN
 #define SR_BUDGET_DPMIN 0.02f
-#define SR_BUDGET_TMAX 8.0f
+#endif
+#ifndef SR_BUDGET_TMAX
+#define SR_BUDGET_TMAX 32.0f
+#endif
 // Objects held in the per-lane budget registers (index 0 is the black hole).
 #define SR_MAX_BUDGET 8
 

@@ -373,10 +373,11 @@ __device__ __forceinline__ void budget_set(Budget& bs, int j, float v) {
         if (jj == j) bs.E[jj] = v;
 }
 
-__device__ __forceinline__ float budget_min(const Budget& bs) {
+__device__ __forceinline__ float budget_min(const Budget& bs, int nb) {
     float m = bs.E[0];
 #pragma unroll
-    for (int j = 1; j <= SR_MAX_BUDGET; j++) m = nmin(m, bs.E[j]);
+    for (int j = 1; j <= SR_MAX_BUDGET; j++)
+        m = nmin(m, bs.E[j]);
     return m;
 }
 
@@ -402,7 +403,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     for (int j = 0; j <= SR_MAX_BUDGET; j++) bs.E[j] = INFINITY;
 #pragma unroll 1
     for (int j = 0; j <= nb; j++) budget_set(bs, j, clearance(sc, j, A, a));
-    bs.m = budget_min(bs);
+    bs.m = budget_min(bs, nb);
     budget_frame(sc, bs, nv, tv);
 }
 
@@ -470,7 +471,8 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
                         if (pA < lo_ || pA > hi_) t1 = -1.0f;
                         return;
                     }
-                    float ta = (lo_ - pA) / dpv, tb = (hi_ - pA) / dpv;
+                    const float inv = __builtin_amdgcn_rcpf(dpv);  // the margin covers its rounding
+                    float ta = (lo_ - pA) * inv, tb = (hi_ - pA) * inv;
                     if (ta > tb) {
                         const float tt = ta;
                         ta = tb;
@@ -510,6 +512,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
 // the chord may reach: their exact tests need the exact chord.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par) {
+    const int nb = sc->num_budget;
     uint32_t spent = 0;
 #pragma unroll
     for (int j = 0; j <= SR_MAX_BUDGET; j++)
@@ -538,7 +541,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
     }
     bs.T = 0.0f;
-    bs.m = budget_min(bs);
+    bs.m = budget_min(bs, nb);
     return reach;
 }
 
