@@ -357,29 +357,17 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // spent are re-anchored (and tested if the chord may reach them). Unused
 // slots hold +inf. (pa, pb)[k] = (nv, tv) . axis of the k-th budgeted
 // cylinder (budget_cyl_mask bit order) for the chord-direction test.
+// E lives in LDS, one column per thread (E[j * 256], conflict-free): the
+// event loop indexes it with the wave-uniform slot j in a compact runtime
+// loop, and the step loop's registers hold only T and m.
+#define SR_E_STRIDE 256
 struct Budget {
-    float E[SR_MAX_BUDGET + 1];
+    float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
-    float pa[SR_MAX_CYLINDERS], pb[SR_MAX_CYLINDERS];
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
 };
-
-// E[j] = v for a wave-uniform slot j (constant register indices: no scratch)
-__device__ __forceinline__ void budget_set(Budget& bs, int j, float v) {
-#pragma unroll
-    for (int jj = 0; jj <= SR_MAX_BUDGET; jj++)
-        if (jj == j) bs.E[jj] = v;
-}
-
-__device__ __forceinline__ float budget_min(const Budget& bs, int nb) {
-    float m = bs.E[0];
-#pragma unroll
-    for (int j = 1; j <= SR_MAX_BUDGET; j++)
-        m = nmin(m, bs.E[j]);
-    return m;
-}
 
 // the orbital frame's projections on the budgeted cylinders' axes
 __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 nv, f3 tv) {
@@ -388,8 +376,8 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
             const f3 ax = ld3(sc->objs[sc->budget_idx[__builtin_ctz(c)]].f + SR_F_AXES + 3);
-            bs.pa[k] = dot(nv, ax);
-            bs.pb[k] = dot(tv, ax);
+            bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] = dot(nv, ax);
+            bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE] = dot(tv, ax);
             c &= c - 1;
         }
     }
@@ -399,11 +387,14 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
-#pragma unroll
-    for (int j = 0; j <= SR_MAX_BUDGET; j++) bs.E[j] = INFINITY;
+    float m = INFINITY;
 #pragma unroll 1
-    for (int j = 0; j <= nb; j++) budget_set(bs, j, clearance(sc, j, A, a));
-    bs.m = budget_min(bs, nb);
+    for (int j = 0; j <= nb; j++) {
+        const float e = clearance(sc, j, A, a);
+        bs.E[j * SR_E_STRIDE] = e;
+        m = nmin(m, e);
+    }
+    bs.m = m;
     budget_frame(sc, bs, nv, tv);
 }
 
@@ -422,7 +413,8 @@ __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restric
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
-            const float ca = a * bs.pa[k] + b * bs.pb[k];
+            const float ca = a * bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] +
+                             b * bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE];
             if (vague || !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd)) par |= 1u << k;
             c &= c - 1;
         }
@@ -513,35 +505,30 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par) {
     const int nb = sc->num_budget;
-    uint32_t spent = 0;
-#pragma unroll
-    for (int j = 0; j <= SR_MAX_BUDGET; j++)
-        if (__ballot(!(bs.T < bs.E[j]))) spent |= 1u << j;
-    if (__ballot(par != 0u)) {  // cylinder k of budget_cyl_mask -> its slot bit
+    uint32_t par_slots = 0;  // cylinder k of budget_cyl_mask -> its slot bit
+    if (par) {
         uint32_t c = (uint32_t)sc->budget_cyl_mask;
-#pragma unroll
-        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
-            if (c) {
-                if (__ballot((par >> k) & 1u)) spent |= 1u << (__builtin_ctz(c) + 1);
-                c &= c - 1;
-            }
-        }
+        for (int k = 0; c; k++, c &= c - 1)
+            if ((par >> k) & 1u) par_slots |= 1u << (__builtin_ctz(c) + 1);
     }
-#pragma unroll
-    for (int j = 0; j <= SR_MAX_BUDGET; j++)
-        if (!((spent >> j) & 1u)) bs.E[j] = bs.E[j] - bs.T;
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
-#ifdef SR_STATS
-    for (uint32_t c = spent; c; c &= c - 1) SR_STAT(14 + __builtin_ctz(c), 1);
-#endif
-    for (uint32_t c = spent; c; c &= c - 1) {
-        const int j = __builtin_ctz(c);
-        budget_set(bs, j, clearance(sc, j, B, a) - perr);
-        if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
+    float m = INFINITY;
+#pragma unroll 1
+    for (int j = 0; j <= nb; j++) {
+        float e = bs.E[j * SR_E_STRIDE];
+        if (__ballot(!(bs.T < e) || ((par_slots >> j) & 1u))) {
+            SR_STAT(14 + j, 1);
+            e = clearance(sc, j, B, a) - perr;
+            if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
+        } else {
+            e = e - bs.T;
+        }
+        bs.E[j * SR_E_STRIDE] = e;
+        m = nmin(m, e);
     }
     bs.T = 0.0f;
-    bs.m = budget_min(bs, nb);
+    bs.m = m;
     return reach;
 }
 
@@ -1164,7 +1151,9 @@ template <bool CULL, bool RECORD>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
+    __shared__ float lds_E[(SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS) * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     Budget bs;
+    bs.E = lds_E + threadIdx.x;
     if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
@@ -1353,7 +1342,7 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 }  // namespace
 
 #ifndef SR_MIN_WAVES_PER_EU
-#define SR_MIN_WAVES_PER_EU 5
+#define SR_MIN_WAVES_PER_EU 6
 #endif
 
 // 1-D grid: launch slot s renders workgroup tile order[s] (costliest first,

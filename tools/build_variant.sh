@@ -7,7 +7,7 @@ PKG=$ROOT/schwarzschild-raytracer_amd
 NAME=$1; shift
 OBJ=$PKG/build/variants/$NAME; OUT=$PKG/lib/variants
 mkdir -p "$OBJ" "$OUT"
-FLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$ROOT/include -I$PKG/csrc -fno-slp-vectorize -DSR_MIN_WAVES_PER_EU=5"
+FLAGS="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$ROOT/include -I$PKG/csrc -fno-slp-vectorize -DSR_MIN_WAVES_PER_EU=6"
 H=/opt/rocm/bin/hipcc
 $H $FLAGS --offload-arch=gfx950 -fno-gpu-rdc "$@" -x hip -c $PKG/csrc/kernels/geodesic.hip -o $OBJ/geodesic.o &
 $H $FLAGS "$@" -c $PKG/csrc/sr_api.cpp -o $OBJ/sr_api.o &
