@@ -1191,6 +1191,96 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         r.ro = B;
         im = i - 1;
     };
+#ifndef SR_DIVERGENT_LOOP
+    // Fast path: every lane runs the same instructions (RK4, chord bound, flag
+    // compares) and the wave takes the slow path only when some lane needs
+    // attention (exit, budget event, forced chord); the reseed check is a
+    // wave-uniform guard. The slow path handles each case per lane.
+    bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
+    for (; r.i < N; r.i++) {
+        const int i = r.i;
+        // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
+        const float4 e = tbl[2 * i];
+        const float g = tbl[2 * i + 1].x;
+        r.steps++;
+        if (__ballot(r.u < fr.u_f)) {
+            if (r.u < fr.u_f) {  // frag:891-912
+                settle_prev(i);
+                f3 q;
+                if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
+                r.nv = nrm(q);
+                if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return ST_FLAT;
+                r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
+                r.u = 1.0f / len(q);
+                r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
+                if (CULL) budget_frame(sc, bs, r.nv, r.tv);
+                force = true;  // the chord starts at the exact r.ro
+            }
+        }
+        // frag:914-919
+        const float h = e.x;
+        const float u = r.u, du = r.du;
+        float un, dun;
+        {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
+            float k1 = du;
+            float l1 = -u * (1.0f - 1.5f * u);
+            float k2 = du + 0.5f * l1 * h;
+            float ua = u + 0.5f * k1 * h;
+            float l2 = -ua * (1.0f - 1.5f * ua);
+            float k3 = du + 0.5f * l2 * h;
+            float ub = u + 0.5f * k2 * h;
+            float l3 = -ub * (1.0f - 1.5f * ub);
+            float k4 = du + l3 * h;
+            float uc = u + k3 * h;
+            float l4 = -uc * (1.0f - 1.5f * uc);
+            un = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
+            dun = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
+        }
+        const bool gone = un < 0.0f;  // frag:921-922 -> get_bg with the previous chord
+        const float rB = __builtin_amdgcn_rcpf(un);
+        float Tn = bs.T;
+        uint32_t par = 0;
+        bool event = every || force;
+        if (CULL) {
+            const float dr = rB - rA;
+            const float pe = point_err(rA, rB);
+            const float Tb = Tn + (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
+            Tn = force ? Tn : Tb;
+            par = chord_parallel(sc, bs, rB * e.z - rA * c1, rB * e.w - rA * s1, pe);
+            event = event || !(Tn < bs.m) || par != 0u;
+        }
+        SR_STAT(0, 1);
+        SR_STAT(13, __popcll(__ballot(1)));
+        if (!__ballot(event || gone)) {  // nothing to do: advance
+            bs.T = Tn;
+            up = r.u;
+            r.u = un;
+            r.du = dun;
+            c2 = c1;
+            s2 = s1;
+            c1 = e.z;
+            s1 = e.w;
+            rA = rB;
+            continue;
+        }
+        if (gone) {
+            settle_prev(i);
+            return ST_BG;
+        }
+        bs.T = Tn;
+        up = r.u;
+        r.u = un;
+        r.du = dun;
+        c2 = c1;
+        s2 = s1;
+        c1 = e.z;
+        s1 = e.w;
+        const float rAold = rA;
+        rA = rB;
+        const bool reseeded = force;
+        force = false;
+        if (!__ballot(event)) continue;
+#else
     for (; r.i < N; r.i++) {
         const int i = r.i;
         // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
@@ -1256,6 +1346,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         SR_STAT(0, 1);
         SR_STAT(13, __popcll(__ballot(1)));
         if (!__ballot(event)) continue;
+#endif
         uint32_t reach = 0xffffffffu;
         if (CULL) {
             // the approximate chord (exact start when materialised)
