@@ -364,23 +364,34 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
+    uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
 };
 
-// the orbital frame's projections on the budgeted cylinders' axes
+// The orbital frame's projections (pa, pb) on the budgeted cylinders' axes.
+// Every chord lies in span(nv, tv), so its direction d has (d . axis)^2 <=
+// pa^2 + pb^2 (Cauchy-Schwarz): when that is below 1 - 2 SR_BUDGET_DPMIN (with
+// a rounding allowance far above the frame's non-orthonormality) no chord of
+// this orbit can be near-parallel to the axis and bit k of bs.cm stays clear:
+// chord_parallel skips the cylinder for this lane.
 __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 nv, f3 tv) {
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
+    uint32_t cm = 0;
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
             const f3 ax = ld3(sc->objs[sc->budget_idx[__builtin_ctz(c)]].f + SR_F_AXES + 3);
-            bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] = dot(nv, ax);
-            bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE] = dot(tv, ax);
+            const float pa = dot(nv, ax), pb = dot(tv, ax);
+            bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] = pa;
+            bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE] = pb;
+            // NaN frames keep the test (the comparison is false)
+            cm |= (uint32_t)(!(pa * pa + pb * pb < 1.0f - 2.0f * SR_BUDGET_DPMIN - 1.0e-3f)) << k;
             c &= c - 1;
         }
     }
+    bs.cm = cm;
 }
 
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv) {
@@ -405,8 +416,9 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 // direction is not known to 0.4%.
 __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restrict__ sc, const Budget& bs, float a,
                                                    float b, float perr) {
+    const uint32_t cm = bs.cm;
+    if (!__ballot(cm != 0u)) return 0u;  // no lane's orbital plane nearly contains an axis (usual case)
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
-    if (!c) return 0u;
     const float dd = a * a + b * b;
     const bool vague = !(perr * perr <= 1.6e-5f * dd);
     uint32_t par = 0;
@@ -415,11 +427,12 @@ __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restric
         if (c) {
             const float ca = a * bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] +
                              b * bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE];
-            if (vague || !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd)) par |= 1u << k;
+            const bool near = vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd);
+            par |= (uint32_t)near << k;
             c &= c - 1;
         }
     }
-    return par;
+    return par & cm;
 }
 
 // Conservative: may the exact chord, within perr of the segment [A, B], come
@@ -1128,6 +1141,48 @@ __device__ __forceinline__ f3 point_near(const Ray& r, float rad, float c, float
 // absolute error bound of point_near / chord components for radii rA, rB
 __device__ __forceinline__ float point_err(float rA, float rB) { return 4.0e-6f * (rA + rB); }
 
+// ddu, frag:336-338
+__device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
+
+// rk4_step, frag:341-355, plus the `u += .x; du += .y` of frag:918-919 (h6 =
+// `delta_phi / 6.`, computed on the host). The u and u' halves of each stage
+// are the same operations on different operands, so they run as packed
+// binary32 pairs (v_pk_mul_f32 / v_pk_add_f32: two correctly rounded results
+// per lane, bit-identical to the scalar expressions):
+//   (ua, k2) = (u, u') + (0.5 (k1, l1)) h      l2 = ddu(ua)
+//   (ub, k3) = (u, u') + (0.5 (k2, l2)) h      l3 = ddu(ub)
+//   (uc, k4) = (u, u') + (k3, l3) h            l4 = ddu(uc)
+//   (u, u') += h6 (((k1, l1) + 2 (k2, l2)) + 2 (k3, l3)) + (k4, l4))
+typedef float v2f __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void rk4_step(float u, float du, float h, float h6, float& un, float& dun) {
+#ifdef SR_SCALAR_RK4
+    const float k1 = du;
+    const float l1 = ddu(u);
+    const float k2 = du + 0.5f * l1 * h;
+    const float l2 = ddu(u + 0.5f * k1 * h);
+    const float k3 = du + 0.5f * l2 * h;
+    const float l3 = ddu(u + 0.5f * k2 * h);
+    const float k4 = du + l3 * h;
+    const float l4 = ddu(u + k3 * h);
+    un = u + h6 * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
+    dun = du + h6 * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
+#else
+    const v2f s0 = {u, du};
+    const v2f hh = {h, h};
+    const v2f q1 = {du, ddu(u)};
+    const v2f p1 = s0 + (0.5f * q1) * hh;
+    const v2f q2 = {p1.y, ddu(p1.x)};
+    const v2f p2 = s0 + (0.5f * q2) * hh;
+    const v2f q3 = {p2.y, ddu(p2.x)};
+    const v2f p3 = s0 + q3 * hh;
+    const v2f q4 = {p3.y, ddu(p3.x)};
+    const v2f hs = {h6, h6};
+    const v2f r = s0 + hs * (((q1 + 2.0f * q2) + 2.0f * q3) + q4);
+    un = r.x;
+    dun = r.y;
+#endif
+}
+
 // The step loop, frag:890-933, from step r.i (entry: r.u = u after step
 // r.i - 1, r.ro / r.rd = that step's chord end and direction).
 //
@@ -1218,24 +1273,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             }
         }
         // frag:914-919
-        const float h = e.x;
-        const float u = r.u, du = r.du;
         float un, dun;
-        {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
-            float k1 = du;
-            float l1 = -u * (1.0f - 1.5f * u);
-            float k2 = du + 0.5f * l1 * h;
-            float ua = u + 0.5f * k1 * h;
-            float l2 = -ua * (1.0f - 1.5f * ua);
-            float k3 = du + 0.5f * l2 * h;
-            float ub = u + 0.5f * k2 * h;
-            float l3 = -ub * (1.0f - 1.5f * ub);
-            float k4 = du + l3 * h;
-            float uc = u + k3 * h;
-            float l4 = -uc * (1.0f - 1.5f * uc);
-            un = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
-            dun = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
-        }
+        rk4_step(r.u, r.du, e.x, e.y, un, dun);
         const bool gone = un < 0.0f;  // frag:921-922 -> get_bg with the previous chord
         const float rB = __builtin_amdgcn_rcpf(un);
         float Tn = bs.T;
@@ -1301,24 +1340,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             reseeded = true;  // new orbital frame: the chord starts at the exact r.ro
         }
         // frag:914-919
-        const float h = e.x;
-        const float u = r.u, du = r.du;
         float un, dun;
-        {  // rk4_step, frag:341-355 (`delta_phi / 6.` is e.y, computed on the host)
-            float k1 = du;
-            float l1 = -u * (1.0f - 1.5f * u);
-            float k2 = du + 0.5f * l1 * h;
-            float ua = u + 0.5f * k1 * h;
-            float l2 = -ua * (1.0f - 1.5f * ua);
-            float k3 = du + 0.5f * l2 * h;
-            float ub = u + 0.5f * k2 * h;
-            float l3 = -ub * (1.0f - 1.5f * ub);
-            float k4 = du + l3 * h;
-            float uc = u + k3 * h;
-            float l4 = -uc * (1.0f - 1.5f * uc);
-            un = u + e.y * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
-            dun = du + e.y * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
-        }
+        rk4_step(r.u, r.du, e.x, e.y, un, dun);
         if (un < 0.0f) {  // frag:921-922 -> get_bg with the previous chord
             settle_prev(i);
             return ST_BG;
