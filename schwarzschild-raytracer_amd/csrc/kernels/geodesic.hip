@@ -348,6 +348,19 @@ __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, 
     return c - 1.8f * SR_MU_QUADRATIC * a;
 }
 
+// Direction-independent part of a budgeted cylinder's clearance: the distance
+// from A to its height slab (0 <= (p - pos) . axes[1] <= height). cyl_test
+// accepts only a point p = o + lambda d with 0 <= lambda <= len, i.e. on the
+// chord up to rounding, whose computed height passes that window, so this
+// bound holds however ill-conditioned the lateral quadratic is (chords nearly
+// parallel to the axis). Same margins as clearance(); -inf without a unit axis.
+__device__ __forceinline__ float clearance_slab(const sr_dev_obj& ob, f3 A, float a) {
+    if (!(ob.mp < INFINITY)) return -INFINITY;
+    const float y = dot(A - ld3(ob.f + SR_F_POS), ld3(ob.f + SR_F_AXES + 3));
+    const float ey = fmaxf(0.0f, fmaxf(-y, y - ob.f[SR_F_P0]));
+    return ey - ob.mp - 1.8f * SR_MU_QUADRATIC * a;
+}
+
 // NaN-propagating minimum: a NaN clearance must force the exact tests.
 __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e : m; }
 
@@ -361,10 +374,15 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // event loop indexes it with the wave-uniform slot j in a compact runtime
 // loop, and the step loop's registers hold only T and m.
 #define SR_E_STRIDE 256
+#define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
+#define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
+#define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
+    float mh;     // min_k of the cylinders' slab budgets H[k] (E[SR_E_SLAB0 + k]): the bound that
+                  // covers chords nearly parallel to an axis
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -384,8 +402,8 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         if (c) {
             const f3 ax = ld3(sc->objs[sc->budget_idx[__builtin_ctz(c)]].f + SR_F_AXES + 3);
             const float pa = dot(nv, ax), pb = dot(tv, ax);
-            bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] = pa;
-            bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE] = pb;
+            bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE] = pa;
+            bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
             // NaN frames keep the test (the comparison is false)
             cm |= (uint32_t)(!(pa * pa + pb * pb < 1.0f - 2.0f * SR_BUDGET_DPMIN - 1.0e-3f)) << k;
             c &= c - 1;
@@ -406,6 +424,18 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         m = nmin(m, e);
     }
     bs.m = m;
+    float mh = INFINITY;
+    uint32_t c = (uint32_t)sc->budget_cyl_mask;
+#pragma unroll
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        if (c) {
+            const float e = clearance_slab(sc->objs[sc->budget_idx[__builtin_ctz(c)]], A, a);
+            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = e;
+            mh = nmin(mh, e);
+            c &= c - 1;
+        }
+    }
+    bs.mh = mh;
     budget_frame(sc, bs, nv, tv);
 }
 
@@ -417,7 +447,6 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restrict__ sc, const Budget& bs, float a,
                                                    float b, float perr) {
     const uint32_t cm = bs.cm;
-    if (!__ballot(cm != 0u)) return 0u;  // no lane's orbital plane nearly contains an axis (usual case)
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
     const float dd = a * a + b * b;
     const bool vague = !(perr * perr <= 1.6e-5f * dd);
@@ -425,8 +454,8 @@ __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restric
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
-            const float ca = a * bs.E[(SR_MAX_BUDGET + 1 + 2 * k) * SR_E_STRIDE] +
-                             b * bs.E[(SR_MAX_BUDGET + 2 + 2 * k) * SR_E_STRIDE];
+            const float ca = a * bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE] +
+                             b * bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE];
             const bool near = vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd);
             par |= (uint32_t)near << k;
             c &= c - 1;
@@ -490,6 +519,10 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
                 slab(yA, yB, ob.f[14]);
                 slab(zA, zB, ob.f[13]);
                 if (t0 > t1 + 1e-6f) return false;
+            } else if (ob.type == SR_OBJECT_CYLINDER) {
+                // the chord must reach the height slab (clearance_slab), in any direction
+                const float hc = ob.f[SR_F_P0];
+                if ((yA < -m && yB < -m) || (yA > hc + m && yB > hc + m)) return false;
             }
         }
         if (ob.type == SR_OBJECT_CYLINDER) {
@@ -512,36 +545,53 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
 
 // Budget event for the chord of this step, known approximately as [A, B]
 // (exact end points within perr; bs.T already charged with it). Slots whose
-// budget is spent, or cylinders the chord may be near-parallel to (par),
-// re-anchor at B (clearance - perr); returns the wave-uniform mask of those
-// the chord may reach: their exact tests need the exact chord.
+// budget is spent re-anchor at B (clearance - perr); returns the
+// wave-uniform mask of those the chord may reach: their exact tests need the
+// exact chord. A budgeted cylinder's E covers chords at least SR_BUDGET_DPMIN
+// off its axis direction; chords that may be closer (par, bit k = cylinder k)
+// are covered by its slab budget H[k] instead, and the slot re-anchors when
+// that is spent too. reanchor_cyl: a new orbital frame (reseed) re-anchors
+// every cylinder slot.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
-                                                 float perr, uint32_t par) {
+                                                 float perr, uint32_t par, bool reanchor_cyl) {
     const int nb = sc->num_budget;
-    uint32_t par_slots = 0;  // cylinder k of budget_cyl_mask -> its slot bit
-    if (par) {
-        uint32_t c = (uint32_t)sc->budget_cyl_mask;
-        for (int k = 0; c; k++, c &= c - 1)
-            if ((par >> k) & 1u) par_slots |= 1u << (__builtin_ctz(c) + 1);
+    const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
+    uint32_t forced = 0;                                 // this lane's slots whose E does not cover the chord
+    {
+        uint32_t c = cyl;
+        for (int k = 0; c; k++, c &= c - 1) {
+            const bool f = reanchor_cyl || (((par >> k) & 1u) && !(bs.T < bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE]));
+            forced |= (uint32_t)f << (__builtin_ctz(c) + 1);
+        }
     }
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
-    float m = INFINITY;
+    float m = INFINITY, mh = INFINITY;
 #pragma unroll 1
     for (int j = 0; j <= nb; j++) {
         float e = bs.E[j * SR_E_STRIDE];
-        if (__ballot(!(bs.T < e) || ((par_slots >> j) & 1u))) {
+        // this slot's cylinder index k, or -1 (wave-uniform)
+        const int k = j > 0 && ((cyl >> (j - 1)) & 1u) ? __builtin_popcount(cyl & ((1u << (j - 1)) - 1u)) : -1;
+        float h = k >= 0 ? bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] : 0.0f;
+        if (__ballot(!(bs.T < e) || ((forced >> j) & 1u))) {
             SR_STAT(14 + j, 1);
             e = clearance(sc, j, B, a) - perr;
+            if (k >= 0) h = clearance_slab(sc->objs[sc->budget_idx[j - 1]], B, a) - perr;
             if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
         } else {
             e = e - bs.T;
+            h = h - bs.T;
         }
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
+        if (k >= 0) {
+            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = h;
+            mh = nmin(mh, h);
+        }
     }
     bs.T = 0.0f;
     bs.m = m;
+    bs.mh = mh;
     return reach;
 }
 
@@ -1206,7 +1256,7 @@ template <bool CULL, bool RECORD>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
-    __shared__ float lds_E[(SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS) * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
+    __shared__ float lds_E[SR_E_ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     Budget bs;
     bs.E = lds_E + threadIdx.x;
     if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv);
@@ -1223,42 +1273,97 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     // the test rays are present (wave-uniform)
     const bool every = !CULL || sc->num_step > 0 || sc->tr_visible;
     // Chord bookkeeping: im = the step whose chord r.ro / r.rd hold; up = u
-    // after step i - 2; (c1, s1) / (c2, s2) = cos / sin phi of steps i - 1 /
-    // i - 2 (step -1: the camera, phi = 0); rA ~ 1 / u after step i - 1.
+    // after step i - 2; rA ~ 1 / u after step i - 1. r.steps = sbase + (steps
+    // begun). In sr_integrate_kernel the step index i is wave-uniform.
     int im = r.i - 1;
     float up = 0.0f;
-    float c1 = 1.0f, s1 = 0.0f, c2 = 1.0f, s2 = 0.0f;
-    if (r.i > 0) {
-        const float4 e1 = tbl[2 * r.i - 2];
-        c1 = e1.z;
-        s1 = e1.w;
-    }
     float rA = __builtin_amdgcn_rcpf(r.u);
+    const int sbase = r.steps - r.i;
+    // {cos phi, sin phi} after step j (step -1: the camera, phi = 0)
+    auto phi_cs = [&](int j) -> f2 {
+        if (j < 0) return F2(1.0f, 0.0f);
+        const float4 t = tbl[2 * j];
+        return F2(t.z, t.w);
+    };
     // materialise the chord of step i - 1 (its end point from r.u, its start
     // from r.ro when that is step i - 2, else from up)
     auto settle_prev = [&](int i) {
         if (im == i - 1) return;
-        f3 A = im == i - 2 ? r.ro : point_at(r, up, c2, s2);
-        f3 B = point_at(r, r.u, c1, s1);
+        const f2 p1 = phi_cs(i - 1);
+        f3 A;
+        if (im == i - 2) {
+            A = r.ro;
+        } else {
+            const f2 p2 = phi_cs(i - 2);
+            A = point_at(r, up, p2.x, p2.y);
+        }
+        f3 B = point_at(r, r.u, p1.x, p1.y);
         f3 delta = B - A;
         float seg = len(delta);
         r.rd = delta / seg;
         r.ro = B;
         im = i - 1;
     };
-#ifndef SR_DIVERGENT_LOOP
-    // Fast path: every lane runs the same instructions (RK4, chord bound, flag
-    // compares) and the wave takes the slow path only when some lane needs
-    // attention (exit, budget event, forced chord); the reseed check is a
-    // wave-uniform guard. The slow path handles each case per lane.
-    bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
-    for (; r.i < N; r.i++) {
-        const int i = r.i;
-        // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
-        const float4 e = tbl[2 * i];
-        const float g = tbl[2 * i + 1].x;
-        r.steps++;
-        if (__ballot(r.u < fr.u_f)) {
+    bool force = false;    // this lane's next chord is charged exactly (new orbital frame)
+    int i = r.i;
+    int checked = -1;      // the step whose reseed check is done
+    for (;;) {
+        if (RECORD) {  // sr_integrate_kernel: every lane starts at step 0, so i is wave-uniform; keep it scalar
+            i = __builtin_amdgcn_readfirstlane(i);
+            checked = __builtin_amdgcn_readfirstlane(checked);
+        }  // (sr_resume_kernel's lanes are unrelated rays at their own steps)
+        // ---- fast loop: RK4, the chord-length bound and the budget compares,
+        // the same instructions on every lane and wave-uniform exits only; the
+        // wave leaves it when some lane needs attention (reseed, exit, budget
+        // event, forced chord) and the slow path below handles step i per lane.
+        // Only numbers leave this loop (lane-mask booleans carried out of it
+        // cost exec-mask bookkeeping on every step); the slow path re-derives
+        // the per-lane conditions from them.
+        float4 e = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float un = 0.0f, dun = 0.0f, rB = 0.0f, Tn = 0.0f;
+        uint32_t par = 0;
+        int reseed = 0;  // wave-uniform
+        for (;;) {
+            if (i >= N) break;
+            if (i != checked && __ballot(r.u < fr.u_f)) {
+                reseed = 1;
+                break;
+            }
+            // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
+            e = tbl[2 * i];
+            const float g = tbl[2 * i + 1].x;
+            rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
+            rB = __builtin_amdgcn_rcpf(un);
+            Tn = bs.T;
+            bool event = every || force;
+            par = 0;
+            if (CULL) {
+                const float dr = rB - rA;
+                const float pe = point_err(rA, rB);
+                const float Tb = Tn + (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
+                Tn = force ? Tn : Tb;
+                if (__ballot(bs.cm != 0u)) {  // some orbital plane nearly contains a cylinder axis
+                    const f2 p1 = phi_cs(i - 1);
+                    par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, pe);
+                }
+                event = event || !(Tn < bs.m) || (par != 0u && !(Tn < bs.mh));
+            }
+            SR_STAT(0, 1);
+            SR_STAT(13, __popcll(__ballot(1)));
+            // un < 0: frag:921-922 -> get_bg with the previous chord
+            if (__ballot(event || un < 0.0f)) break;
+            bs.T = Tn;
+            up = r.u;
+            r.u = un;
+            r.du = dun;
+            rA = rB;
+            i++;
+        }
+        if (i >= N) break;
+        r.i = i;
+        r.steps = sbase + i + 1;
+        if (reseed) {
+            checked = i;
             if (r.u < fr.u_f) {  // frag:891-912
                 settle_prev(i);
                 f3 q;
@@ -1271,38 +1376,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (CULL) budget_frame(sc, bs, r.nv, r.tv);
                 force = true;  // the chord starts at the exact r.ro
             }
+            continue;  // step i with the new frames
         }
-        // frag:914-919
-        float un, dun;
-        rk4_step(r.u, r.du, e.x, e.y, un, dun);
-        const bool gone = un < 0.0f;  // frag:921-922 -> get_bg with the previous chord
-        const float rB = __builtin_amdgcn_rcpf(un);
-        float Tn = bs.T;
-        uint32_t par = 0;
+        // ---- slow path of step i
         bool event = every || force;
-        if (CULL) {
-            const float dr = rB - rA;
-            const float pe = point_err(rA, rB);
-            const float Tb = Tn + (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
-            Tn = force ? Tn : Tb;
-            par = chord_parallel(sc, bs, rB * e.z - rA * c1, rB * e.w - rA * s1, pe);
-            event = event || !(Tn < bs.m) || par != 0u;
-        }
-        SR_STAT(0, 1);
-        SR_STAT(13, __popcll(__ballot(1)));
-        if (!__ballot(event || gone)) {  // nothing to do: advance
-            bs.T = Tn;
-            up = r.u;
-            r.u = un;
-            r.du = dun;
-            c2 = c1;
-            s2 = s1;
-            c1 = e.z;
-            s1 = e.w;
-            rA = rB;
-            continue;
-        }
-        if (gone) {
+        if (CULL) event = event || !(Tn < bs.m) || (par != 0u && !(Tn < bs.mh));
+        if (un < 0.0f) {
             settle_prev(i);
             return ST_BG;
         }
@@ -1310,119 +1389,70 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         up = r.u;
         r.u = un;
         r.du = dun;
-        c2 = c1;
-        s2 = s1;
-        c1 = e.z;
-        s1 = e.w;
         const float rAold = rA;
         rA = rB;
         const bool reseeded = force;
         force = false;
-        if (!__ballot(event)) continue;
-#else
-    for (; r.i < N; r.i++) {
-        const int i = r.i;
-        // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
-        const float4 e = tbl[2 * i];
-        const float g = tbl[2 * i + 1].x;
-        r.steps++;
-        bool reseeded = false;
-        if (r.u < fr.u_f) {  // frag:891-912
-            settle_prev(i);
-            f3 q;
-            if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
-            r.nv = nrm(q);
-            if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return ST_FLAT;
-            r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
-            r.u = 1.0f / len(q);
-            r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-            if (CULL) budget_frame(sc, bs, r.nv, r.tv);
-            reseeded = true;  // new orbital frame: the chord starts at the exact r.ro
-        }
-        // frag:914-919
-        float un, dun;
-        rk4_step(r.u, r.du, e.x, e.y, un, dun);
-        if (un < 0.0f) {  // frag:921-922 -> get_bg with the previous chord
-            settle_prev(i);
-            return ST_BG;
-        }
-        const float rB = __builtin_amdgcn_rcpf(un);
-        bool event = every || reseeded;
-        uint32_t par = 0;
-        if (CULL && !reseeded) {
-            const float dr = rB - rA;
-            const float pe = point_err(rA, rB);
-            bs.T += (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
-            par = chord_parallel(sc, bs, rB * e.z - rA * c1, rB * e.w - rA * s1, pe);
-            event = event || !(bs.T < bs.m) || par != 0u;
-        }
-        // advance: step i's u becomes the current one
-        up = r.u;
-        r.u = un;
-        r.du = dun;
-        c2 = c1;
-        s2 = s1;
-        c1 = e.z;
-        s1 = e.w;
-        const float rAold = rA;
-        rA = rB;
-        SR_STAT(0, 1);
-        SR_STAT(13, __popcll(__ballot(1)));
-        if (!__ballot(event)) continue;
-#endif
-        uint32_t reach = 0xffffffffu;
-        if (CULL) {
-            // the approximate chord (exact start when materialised)
-            const bool exact_start = im == i - 1;
-            const f3 Ap = exact_start ? r.ro : point_near(r, rAold, c2, s2);
-            const f3 Bp = point_near(r, rB, e.z, e.w);
-            const float pe = point_err(exact_start ? 0.0f : rAold, rB);
-            if (reseeded) {  // chord not charged yet
-                const f3 dv = Bp - Ap;
-                bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
-                par = ~0u;  // the frame changed: the cylinders' direction test is redone exactly
-            }
-            SR_STAT(1, 1);
+        do {  // `break`: on to step i + 1
+            if (!__ballot(event)) break;
+            uint32_t reach = 0xffffffffu;
+            const f2 p1 = phi_cs(i - 1);
+            if (CULL) {
+                // the approximate chord (exact start when materialised)
+                const bool exact_start = im == i - 1;
+                const f3 Ap = exact_start ? r.ro : point_near(r, rAold, p1.x, p1.y);
+                const f3 Bp = point_near(r, rB, e.z, e.w);
+                const float pe = point_err(exact_start ? 0.0f : rAold, rB);
+                if (reseeded) {  // chord not charged yet
+                    const f3 dv = Bp - Ap;
+                    bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
+                }
+                SR_STAT(1, 1);
 #ifdef SR_STATS
-            r.ev++;
+                r.ev++;
 #endif
-            reach = budget_event(sc, bs, Ap, Bp, pe, par);
+                // a new frame (reseed): the cylinders' direction tests start over
+                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded);
 #ifdef SR_STATS
-            for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
+                for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
 #pragma unroll
-            for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] += (reach >> j) & 1u;
+                for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] += (reach >> j) & 1u;
 #endif
-            if (!__ballot(reach != 0u || every)) continue;
+                if (!__ballot(reach != 0u || every)) break;
 #ifdef SR_STATS_FIRE
-            bs.fires++;
+                bs.fires++;
 #endif
-        }
-        // frag:924-930: the exact chord of step i
+            }
+            // frag:924-930: the exact chord of step i
 #ifdef SR_STATS
-        r.mat++;
+            r.mat++;
 #endif
-        f3 prev = im == i - 1 ? r.ro : point_at(r, up, c2, s2);
-        r.ro = point_at(r, r.u, e.z, e.w);
-        im = i;
-        f3 delta = r.ro - prev;
-        float seg = len(delta);
-        r.rd = delta / seg;
-        hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
-        if (hit.slot != SLOT_NONE) {
-            const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
-            if (op == OP_ZERO) continue;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
-            if (!RECORD) return ST_HIT;
-            const int f = PS_HIT0 + PS_HIT_STRIDE * log.n;
-            log.ps.put3(f, log.id, hit.p);
-            log.ps.puti(f + 3, log.id, hit.slot * 8 + hit.face);
-            log.ps.put3(f + 4, log.id, r.rd);
-            log.ps.puti(f + 7, log.id, r.steps);  // the ray's step count if this hit ends it
-            log.n++;
-            if (op == OP_OPAQUE) return ST_HIT;
-            if (log.n == SR_PS_HITS) return ST_MORE;
-        }
+            f3 prev = im == i - 1 ? r.ro : point_at(r, up, p1.x, p1.y);
+            r.ro = point_at(r, r.u, e.z, e.w);
+            im = i;
+            f3 delta = r.ro - prev;
+            float seg = len(delta);
+            r.rd = delta / seg;
+            hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
+            if (hit.slot != SLOT_NONE) {
+                const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
+                if (op == OP_ZERO) break;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
+                if (!RECORD) return ST_HIT;
+                const int f = PS_HIT0 + PS_HIT_STRIDE * log.n;
+                log.ps.put3(f, log.id, hit.p);
+                log.ps.puti(f + 3, log.id, hit.slot * 8 + hit.face);
+                log.ps.put3(f + 4, log.id, r.rd);
+                log.ps.puti(f + 7, log.id, r.steps);  // the ray's step count if this hit ends it
+                log.n++;
+                if (op == OP_OPAQUE) return ST_HIT;
+                if (log.n == SR_PS_HITS) return ST_MORE;
+            }
+        } while (false);
+        i++;
     }
-    settle_prev(r.i);
+    r.i = N;
+    r.steps = sbase + N;
+    settle_prev(N);
     return ST_BG;
 }
 

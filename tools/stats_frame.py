@@ -20,6 +20,7 @@ def main():
     ap.add_argument("lib")
     ap.add_argument("--scene", default="tex")
     ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -63,6 +64,8 @@ def main():
     lib.sr_debug_wave_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     assert lib.sr_debug_wave_times(tb, nw) == 0
     t = np.frombuffer(tb, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
+    if args.save:
+        np.save(args.save, t)
     wid = np.arange(nw)[t[:, 1] > 0]
     t = t[t[:, 1] > 0]
     t0 = t[:, 0].min()
