@@ -552,42 +552,78 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
 // are covered by its slab budget H[k] instead, and the slot re-anchors when
 // that is spent too. reanchor_cyl: a new orbital frame (reseed) re-anchors
 // every cylinder slot.
+// Two phases: every budget is read at once and compared (unrolled over the
+// slot capacity, no per-slot branches or LDS round trips), then only the
+// slots some lane has spent - usually one - run their clearance and reach
+// tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl) {
+    constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
-    uint32_t forced = 0;                                 // this lane's slots whose E does not cover the chord
+    const float T = bs.T;
+    float e[NS], h[SR_MAX_CYLINDERS];
+#pragma unroll
+    for (int j = 0; j < NS; j++) e[j] = bs.E[j * SR_E_STRIDE];
+#pragma unroll
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) h[k] = bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE];
+    uint32_t forced = 0;  // this lane's slots whose E does not cover the chord
     {
         uint32_t c = cyl;
-        for (int k = 0; c; k++, c &= c - 1) {
-            const bool f = reanchor_cyl || (((par >> k) & 1u) && !(bs.T < bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE]));
-            forced |= (uint32_t)f << (__builtin_ctz(c) + 1);
+#pragma unroll
+        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+            if (c) {
+                const bool f = reanchor_cyl || (((par >> k) & 1u) && !(T < h[k]));
+                forced |= (uint32_t)f << (__builtin_ctz(c) + 1);
+                c &= c - 1;
+            }
         }
     }
+    uint32_t spent = 0;  // wave-uniform: slots some lane has spent
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+        if (__ballot(!(T < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
+    spent &= (2u << nb) - 1u;
+    // the others run on: charge them the path since the last event
+    float m = INFINITY, mh = INFINITY;
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        if (j <= nb && !((spent >> j) & 1u)) {
+            const float v = e[j] - T;
+            bs.E[j * SR_E_STRIDE] = v;
+            m = nmin(m, v);
+        }
+    }
+    {
+        uint32_t c = cyl;
+#pragma unroll
+        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+            if (c) {
+                if (!((spent >> (__builtin_ctz(c) + 1)) & 1u)) {
+                    const float v = h[k] - T;
+                    bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = v;
+                    mh = nmin(mh, v);
+                }
+                c &= c - 1;
+            }
+        }
+    }
+    // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
-    float m = INFINITY, mh = INFINITY;
-#pragma unroll 1
-    for (int j = 0; j <= nb; j++) {
-        float e = bs.E[j * SR_E_STRIDE];
-        // this slot's cylinder index k, or -1 (wave-uniform)
-        const int k = j > 0 && ((cyl >> (j - 1)) & 1u) ? __builtin_popcount(cyl & ((1u << (j - 1)) - 1u)) : -1;
-        float h = k >= 0 ? bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] : 0.0f;
-        if (__ballot(!(bs.T < e) || ((forced >> j) & 1u))) {
-            SR_STAT(14 + j, 1);
-            e = clearance(sc, j, B, a) - perr;
-            if (k >= 0) h = clearance_slab(sc->objs[sc->budget_idx[j - 1]], B, a) - perr;
-            if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
-        } else {
-            e = e - bs.T;
-            h = h - bs.T;
+    for (uint32_t w = spent; w; w &= w - 1) {
+        const int j = __builtin_ctz(w);
+        SR_STAT(14 + j, 1);
+        const float v = clearance(sc, j, B, a) - perr;
+        bs.E[j * SR_E_STRIDE] = v;
+        m = nmin(m, v);
+        if (j > 0 && ((cyl >> (j - 1)) & 1u)) {
+            const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
+            const float vh = clearance_slab(sc->objs[sc->budget_idx[j - 1]], B, a) - perr;
+            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
+            mh = nmin(mh, vh);
         }
-        bs.E[j * SR_E_STRIDE] = e;
-        m = nmin(m, e);
-        if (k >= 0) {
-            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = h;
-            mh = nmin(mh, h);
-        }
+        if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
     }
     bs.T = 0.0f;
     bs.m = m;
