@@ -1340,67 +1340,19 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         r.ro = B;
         im = i - 1;
     };
-    bool force = false;    // this lane's next chord is charged exactly (new orbital frame)
+    bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
     int i = r.i;
-    int checked = -1;      // the step whose reseed check is done
     for (;;) {
-        if (RECORD) {  // sr_integrate_kernel: every lane starts at step 0, so i is wave-uniform; keep it scalar
-            i = __builtin_amdgcn_readfirstlane(i);
-            checked = __builtin_amdgcn_readfirstlane(checked);
-        }  // (sr_resume_kernel's lanes are unrelated rays at their own steps)
-        // ---- fast loop: RK4, the chord-length bound and the budget compares,
-        // the same instructions on every lane and wave-uniform exits only; the
-        // wave leaves it when some lane needs attention (reseed, exit, budget
-        // event, forced chord) and the slow path below handles step i per lane.
-        // Only numbers leave this loop (lane-mask booleans carried out of it
-        // cost exec-mask bookkeeping on every step); the slow path re-derives
-        // the per-lane conditions from them.
-        float4 e = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        float un = 0.0f, dun = 0.0f, rB = 0.0f, Tn = 0.0f;
-        uint32_t par = 0;
-        int reseed = 0;  // wave-uniform
-        for (;;) {
-            if (i >= N) break;
-            if (i != checked && __ballot(r.u < fr.u_f)) {
-                reseed = 1;
-                break;
-            }
-            // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -} of step i (wave-uniform)
-            e = tbl[2 * i];
-            const float g = tbl[2 * i + 1].x;
-            rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
-            rB = __builtin_amdgcn_rcpf(un);
-            Tn = bs.T;
-            bool event = every || force;
-            par = 0;
-            if (CULL) {
-                const float dr = rB - rA;
-                const float pe = point_err(rA, rB);
-                const float Tb = Tn + (__builtin_amdgcn_sqrtf(dr * dr + rA * rB * g) * 1.0001f + pe) * SR_PATH_SLACK;
-                Tn = force ? Tn : Tb;
-                if (__ballot(bs.cm != 0u)) {  // some orbital plane nearly contains a cylinder axis
-                    const f2 p1 = phi_cs(i - 1);
-                    par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, pe);
-                }
-                event = event || !(Tn < bs.m) || (par != 0u && !(Tn < bs.mh));
-            }
-            SR_STAT(0, 1);
-            SR_STAT(13, __popcll(__ballot(1)));
-            // un < 0: frag:921-922 -> get_bg with the previous chord
-            if (__ballot(event || un < 0.0f)) break;
-            bs.T = Tn;
-            up = r.u;
-            r.u = un;
-            r.du = dun;
-            rA = rB;
-            i++;
-        }
+        if (RECORD) i = __builtin_amdgcn_readfirstlane(i);  // every lane started at step 0: keep i scalar
+        // (sr_resume_kernel's lanes are unrelated rays at their own steps)
         if (i >= N) break;
-        r.i = i;
-        r.steps = sbase + i + 1;
-        if (reseed) {
-            checked = i;
-            if (r.u < fr.u_f) {  // frag:891-912
+        // frag:891-912, the top of step i (the fast loop below leaves a step
+        // early whenever some lane's u drops below u_f, so this is where
+        // every reseed happens)
+        if (__ballot(r.u < fr.u_f)) {
+            if (r.u < fr.u_f) {
+                r.i = i;
+                r.steps = sbase + i + 1;
                 settle_prev(i);
                 f3 q;
                 if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
@@ -1412,15 +1364,61 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (CULL) budget_frame(sc, bs, r.nv, r.tv);
                 force = true;  // the chord starts at the exact r.ro
             }
-            continue;  // step i with the new frames
         }
+        // ---- fast loop: RK4, the chord-length bound and one compare per
+        // step, the same instructions on every lane and wave-uniform exits
+        // only. The wave leaves with step i computed but not applied when
+        // some lane needs attention: a budget event (Tn >= its limit; the
+        // limit is -inf while every chord is tested or this lane's chord is
+        // forced), an exit (u < 0) or a reseed at the next step (u < u_f).
+        // Only numbers leave the loop (lane-mask booleans carried out of it
+        // cost exec-mask bookkeeping on every step).
+        const float lim0 = (every || force) ? -INFINITY : bs.m;
+        const float4* __restrict__ tp = tbl + 2 * i;  // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -}
+        float4 e;
+        float un, dun, rB, Tn, lim;
+        uint32_t par;
+        for (;;) {
+            e = tp[0];  // wave-uniform scalar loads
+            const float g = tp[1].x;
+            rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
+            rB = __builtin_amdgcn_rcpf(un);
+            Tn = bs.T;
+            lim = lim0;
+            par = 0;
+            if (CULL) {
+                // chord length bound: sqrt(dr^2 + rA rB g) (1 + 1e-4) + point_err, times the
+                // path slack (bounds, not reference arithmetic: FMA allowed)
+                const float dr = rB - rA;
+                const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * g));
+                Tn = __builtin_fmaf(rA + rB, 4.0e-6f * SR_PATH_SLACK, __builtin_fmaf(sq, 1.0001f * SR_PATH_SLACK, Tn));
+                if (__ballot(bs.cm != 0u)) {  // some orbital plane nearly contains a cylinder axis
+                    const f2 p1 = phi_cs(i - 1);
+                    par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));
+                    if (par) lim = nmin(lim, bs.mh);
+                }
+            }
+            SR_STAT(0, 1);
+            SR_STAT(13, __popcll(__ballot(1)));
+            // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
+            if (__ballot(!(Tn < lim) || un < fr.u_f)) break;
+            bs.T = Tn;
+            up = r.u;
+            r.u = un;
+            r.du = dun;
+            rA = rB;
+            tp += 2;
+            if (++i >= N) break;
+        }
+        if (i >= N) break;
         // ---- slow path of step i
-        bool event = every || force;
-        if (CULL) event = event || !(Tn < bs.m) || (par != 0u && !(Tn < bs.mh));
+        r.i = i;
+        r.steps = sbase + i + 1;
         if (un < 0.0f) {
             settle_prev(i);
             return ST_BG;
         }
+        const bool event = !(Tn < lim);
         bs.T = Tn;
         up = r.u;
         r.u = un;
@@ -1439,7 +1437,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 const f3 Ap = exact_start ? r.ro : point_near(r, rAold, p1.x, p1.y);
                 const f3 Bp = point_near(r, rB, e.z, e.w);
                 const float pe = point_err(exact_start ? 0.0f : rAold, rB);
-                if (reseeded) {  // chord not charged yet
+                if (reseeded) {  // new frame: the step's bound used the old radius; charge the chord itself
                     const f3 dv = Bp - Ap;
                     bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
                 }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--scene", default="tex")
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
+    ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080], help="render only rows [a, b) (waves alone on the chip)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -44,9 +45,10 @@ def main():
     params = abi.default_params(max_steps=args.max_steps, percent_black=-1.0)
     buf = (C.c_ulonglong * 32)()
     lib.sr_debug_stats(buf)  # clear
-    r.render(cam, params, 1920, 1080)  # first frame: centre-out launch order
+    ra, rb = args.rows
+    r.render(cam, params, 1920, 1080, ra, rb)  # first frame: centre-out launch order
     lib.sr_debug_stats(buf)  # clear
-    r.render(cam, params, 1920, 1080)  # steady state: cost-ordered launch
+    r.render(cam, params, 1920, 1080, ra, rb)  # steady state: cost-ordered launch
     assert lib.sr_debug_stats(buf) == 0
     def name(k):
         if k in NAMES:
