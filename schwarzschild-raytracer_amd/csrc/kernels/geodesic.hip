@@ -101,6 +101,32 @@ __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
 #define SR_STAT(k, v) ((void)0)
 #endif
 
+#ifdef SR_PROF
+// Measurement builds only (tools/prof_waves.py): per-wave shader-clock cycles
+// by section of the step loop, wave-uniform accumulators (no per-lane state,
+// so the build keeps the production register allocation as far as possible).
+//   0 fast loop  1 reseeds  2 slow-path entry + approximate chord  3 budget events phase 1
+//   4 exact chord + intersect  5 hit classification + log  6 budget events phase 2  7 wave total
+#define SR_PROF_N 8
+__device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
+#define SR_PT(k)                                                      \
+    do {                                                              \
+        const unsigned t_ = (unsigned)clock64();                      \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[k] += t_ - prof_t_; \
+        prof_t_ = t_;                                                 \
+    } while (0)
+// the same inside budget_event (accumulators reached through the Budget)
+#define SR_PTB(k)                                                     \
+    do {                                                              \
+        const unsigned t_ = (unsigned)clock64();                      \
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[k] += t_ - *bs.pt; \
+        *bs.pt = t_;                                                  \
+    } while (0)
+#else
+#define SR_PT(k) ((void)0)
+#define SR_PTB(k) ((void)0)
+#endif
+
 // ---- primitive tests: return the reference's is_hit and fill p ------------
 // sphere_intersect, frag:457-478
 __device__ __forceinline__ bool sphere_test(f3 o, f3 d, f3 c, float r, float max_lambda, f3& p) {
@@ -386,6 +412,10 @@ struct Budget {
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
+#ifdef SR_PROF
+    unsigned* prof;
+    unsigned* pt;
+#endif
 };
 
 // The orbital frame's projections (pa, pb) on the budgeted cylinders' axes.
@@ -608,6 +638,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             }
         }
     }
+    SR_PTB(3);
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
@@ -1119,6 +1150,9 @@ struct Ray {
     f3 ro, rd, nv, tv;
     float u, du;
     int i, steps;
+#ifdef SR_PROF
+    unsigned* prof;  // the wave's 8 section accumulators in LDS
+#endif
 #ifdef SR_STATS
     int ev, mat;  // budget events, exact chords (measurement builds)
     int rc[SR_MAX_BUDGET + 1];
@@ -1342,6 +1376,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     };
     bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
     int i = r.i;
+#ifdef SR_PROF
+    unsigned prof_t_ = (unsigned)clock64();
+    bs.prof = r.prof;
+    bs.pt = &prof_t_;
+#endif
     for (;;) {
         if (RECORD) i = __builtin_amdgcn_readfirstlane(i);  // every lane started at step 0: keep i scalar
         // (sr_resume_kernel's lanes are unrelated rays at their own steps)
@@ -1349,6 +1388,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // frag:891-912, the top of step i (the fast loop below leaves a step
         // early whenever some lane's u drops below u_f, so this is where
         // every reseed happens)
+        SR_PT(2);
         if (__ballot(r.u < fr.u_f)) {
             if (r.u < fr.u_f) {
                 r.i = i;
@@ -1364,6 +1404,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (CULL) budget_frame(sc, bs, r.nv, r.tv);
                 force = true;  // the chord starts at the exact r.ro
             }
+            SR_PT(1);
         }
         // ---- fast loop: RK4, the chord-length bound and one compare per
         // step, the same instructions on every lane and wave-uniform exits
@@ -1374,13 +1415,23 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // Only numbers leave the loop (lane-mask booleans carried out of it
         // cost exec-mask bookkeeping on every step).
         const float lim0 = (every || force) ? -INFINITY : bs.m;
+        // some lane's orbital plane nearly contains a budgeted cylinder's axis
+        // (bs.cm changes only at reseeds, outside the fast loop)
+        const bool any_cm = CULL && __ballot(bs.cm != 0u);
         const float4* __restrict__ tp = tbl + 2 * i;  // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -}
         float4 e;
         float un, dun, rB, Tn, lim;
         uint32_t par;
         for (;;) {
+#ifdef SR_EXP_VTABLE  // experiment: table through the vector memory path (keeps the scalar cache for scene data)
+            int vz_;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(vz_));
+            e = tp[vz_];
+            const float g = tp[vz_ + 1].x;
+#else
             e = tp[0];  // wave-uniform scalar loads
             const float g = tp[1].x;
+#endif
             rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
             rB = __builtin_amdgcn_rcpf(un);
             Tn = bs.T;
@@ -1392,7 +1443,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 const float dr = rB - rA;
                 const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * g));
                 Tn = __builtin_fmaf(rA + rB, 4.0e-6f * SR_PATH_SLACK, __builtin_fmaf(sq, 1.0001f * SR_PATH_SLACK, Tn));
-                if (__ballot(bs.cm != 0u)) {  // some orbital plane nearly contains a cylinder axis
+                if (any_cm) {
                     const f2 p1 = phi_cs(i - 1);
                     par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));
                     if (par) lim = nmin(lim, bs.mh);
@@ -1407,9 +1458,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             r.u = un;
             r.du = dun;
             rA = rB;
+#ifndef SR_EXP_CONST_TABLE  // timing experiment only: every step reads entry 0 (wrong output)
             tp += 2;
+#endif
             if (++i >= N) break;
         }
+        SR_PT(0);
         if (i >= N) break;
         // ---- slow path of step i
         r.i = i;
@@ -1446,7 +1500,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.ev++;
 #endif
                 // a new frame (reseed): the cylinders' direction tests start over
+                SR_PT(2);
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded);
+                SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
 #pragma unroll
@@ -1468,8 +1524,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             float seg = len(delta);
             r.rd = delta / seg;
             hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
+            SR_PT(4);
             if (hit.slot != SLOT_NONE) {
                 const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
+                SR_PT(5);
                 if (op == OP_ZERO) break;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
                 if (!RECORD) return ST_HIT;
                 const int f = PS_HIT0 + PS_HIT_STRIDE * log.n;
@@ -1547,6 +1605,11 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
 #endif
     Pix q;
     int steps = 0;
+#ifdef SR_PROF
+    __shared__ unsigned prof_lds[4][SR_PROF_N];
+    if ((threadIdx.x & 63) < SR_PROF_N) prof_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
+    const unsigned long long prof_t0 = clock64();
+#endif
     if (pixel_of(fr, block, threadIdx.x, q)) {
         const size_t id = (size_t)block * 256 + threadIdx.x;
         Tex tx;
@@ -1558,6 +1621,9 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
         Ray r;
         Hit hit;
         int st = init_pixel(fr, q, r);
+#ifdef SR_PROF
+        r.prof = prof_lds[threadIdx.x >> 6];
+#endif
         if (st < 0) st = integrate<CULL, true>(sc, segs, tbl, fr, tx, r, hit, log);
         ps.puti(PS_STATUS, id, st);
         ps.puti(PS_STEPS, id, r.steps);
@@ -1599,6 +1665,18 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
             rec[2] = (unsigned long long)sm;
             rec[3] = em;
             for (int j = 0; j <= SR_MAX_BUDGET; j++) rec[4 + j] = (unsigned long long)rcm[j];
+        }
+    }
+#endif
+#ifdef SR_PROF
+    {
+        const int w = block * 4 + (int)(threadIdx.x >> 6);
+        int sm = steps;
+        for (int off = 32; off > 0; off >>= 1) sm = max(sm, __shfl_xor(sm, off));
+        if ((threadIdx.x & 63) == 0 && w < (1 << 17)) {
+            unsigned long long* rec = sr_prof + (size_t)SR_PROF_N * w;
+            for (int k = 0; k < SR_PROF_N - 1; k++) rec[k] = prof_lds[threadIdx.x >> 6][k];
+            rec[SR_PROF_N - 1] = (clock64() - prof_t0) | ((unsigned long long)sm << 48);
         }
     }
 #endif
@@ -1774,6 +1852,17 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }
+
+#ifdef SR_PROF
+extern "C" int sr_debug_prof(unsigned long long* out, int n_waves) {
+    if (n_waves < 0 || n_waves > (1 << 17)) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_prof), SR_PROF_N * (size_t)n_waves * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -3;
+    return 0;
+}
+#endif
 
 #ifdef SR_STATS
 // Measurement builds only: read (and clear) the kernel's event counters.
