@@ -107,7 +107,7 @@ __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
 // so the build keeps the production register allocation as far as possible).
 //   0 fast loop  1 reseeds  2 slow-path entry + approximate chord  3 budget events phase 1
 //   4 exact chord + intersect  5 hit classification + log  6 budget events phase 2  7 wave total
-#define SR_PROF_N 8
+#define SR_PROF_N 16  // 0-6 sections, 7 wave total | max steps << 48, 8-15 re-anchors of budget slots 0-7
 __device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
 #define SR_PT(k)                                                      \
     do {                                                              \
@@ -645,6 +645,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
         SR_STAT(14 + j, 1);
+#ifdef SR_PROF
+        if (j < 8 && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[8 + j] += 1;
+#endif
         const float v = clearance(sc, j, B, a) - perr;
         bs.E[j * SR_E_STRIDE] = v;
         m = nmin(m, v);
@@ -1675,8 +1678,8 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
         for (int off = 32; off > 0; off >>= 1) sm = max(sm, __shfl_xor(sm, off));
         if ((threadIdx.x & 63) == 0 && w < (1 << 17)) {
             unsigned long long* rec = sr_prof + (size_t)SR_PROF_N * w;
-            for (int k = 0; k < SR_PROF_N - 1; k++) rec[k] = prof_lds[threadIdx.x >> 6][k];
-            rec[SR_PROF_N - 1] = (clock64() - prof_t0) | ((unsigned long long)sm << 48);
+            for (int k = 0; k < SR_PROF_N; k++) rec[k] = prof_lds[threadIdx.x >> 6][k];
+            rec[7] = (clock64() - prof_t0) | ((unsigned long long)sm << 48);
         }
     }
 #endif

@@ -47,9 +47,9 @@ def main():
         r.render(cam, params, 1920, 1080, a, b)
     torch.cuda.synchronize()
     nw = ((1920 + 15) // 16) * ((b - a + 15) // 16) * 4
-    buf = (C.c_ulonglong * (8 * nw))()
+    buf = (C.c_ulonglong * (16 * nw))()
     assert lib.sr_debug_prof(buf, nw) == 0
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.int64)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
     total = t[:, 7] & ((1 << 48) - 1)
     steps = t[:, 7] >> 48
     ok = total > 0
@@ -57,12 +57,13 @@ def main():
     sums = t[ok, :7].sum(0)
     out["cycles_by_section_all_waves"] = {k: int(v) for k, v in zip(SECTIONS, sums)}
     out["cycles_total_all_waves"] = int(total[ok].sum())
+    out["reanchors_by_slot_all_waves"] = [int(v) for v in t[ok, 8:16].sum(0)]
     gx = (1920 + 15) // 16
     top = np.argsort(-total)[: args.top]
     out["slowest"] = [
         {"wave": int(w), "block_xy": [int(w // 4 % gx), int(w // 4 // gx)], "steps": int(steps[w]),
          "total_cycles": int(total[w]), "cycles_per_step": round(float(total[w]) / max(1, int(steps[w])), 1),
-         **{k: int(v) for k, v in zip(SECTIONS, t[w, :7])}}
+         **{k: int(v) for k, v in zip(SECTIONS, t[w, :7])}, "reanchors_by_slot": [int(v) for v in t[w, 8:16]]}
         for w in top]
     print(json.dumps(out, indent=1))
     r.close()
