@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
+    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
     return ap.parse_args()
 
 
@@ -106,6 +107,8 @@ def main():
     torch.cuda.synchronize(dev)
     sigma_steps_frame = int(steps_full.sum().item())
     sigma_steps_mine = int(steps_full[rows_mine].sum().item())
+    # the 16-row band of workgroup tiles holding the frame's longest ray
+    band_row = int(steps_full.max(dim=1).values.argmax().item()) // 16 * 16
     del steps_full
 
     for _ in range(args.warmup):
@@ -150,6 +153,33 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     mpix_s = W * H * args.steps / elapsed / 1e6
 
+    # Critical path (untimed, after the timed regions): that band rendered on
+    # its own (~120 workgroups, under one wave per SIMD), on a second context
+    # so the frame's launch-order state stays untouched. Its time is the
+    # slowest waves' latency without contention.
+    critical = None
+    if rank == 0 and world == 1:
+        rb = pkg.Renderer(local)
+        rb.set_scene(scene)
+        rb.set_background(sc.skybox(2048, 1024))
+        rb.set_texture_array(arr)
+        rb.set_culling(not args.no_cull)
+        band = (band_row, min(H, band_row + 16))
+        for _ in range(2):
+            rb.render(cam, params, W, H, *band, stream=stream)
+        times = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            rb.render(cam, params, W, H, *band, stream=stream)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            times.append(e0.elapsed_time(e1))
+        rb.close()
+        band_ms = sorted(times)[len(times) // 2]
+        critical = {"band_rows": list(band), "band_ms": round(band_ms, 4),
+                    "frac_of_frame": round(band_ms / kernel_ms, 3)}
+
     if rank == 0:
         # roofline of the dominant kernel (sr_integrate_kernel: ray generation,
         # the step loop and every intersection test), on rank 0's launch
@@ -166,6 +196,15 @@ def main():
                     traffic = rec.get("hbm_bytes_per_launch")
             except Exception:  # noqa: BLE001
                 traffic = None
+        pmc = None
+        pj = Path(args.pmc_json)
+        if pj.exists():
+            try:
+                rec = json.loads(pj.read_text())
+                if rec.get("width") == W and rec.get("height") == H and rec.get("max_steps") == N and world == 1:
+                    pmc = {k: rec[k] for k in ("valu_busy", "salu_per_valu", "source") if k in rec}
+            except Exception:  # noqa: BLE001
+                pmc = None
         roofline = {
             "bound": "valu",
             "kernel": "sr_integrate_kernel",
@@ -187,6 +226,13 @@ def main():
                 "flop_per_frame": frame_flop,
                 "frac": round(frame_flop / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
             },
+            # algorithmic = the reference loop's work; culling
+            # executes a fraction of it, so frac can approach or pass 1. The
+            # frame is bounded by the latency of its longest rays' waves:
+            # critical_path = their band alone; pmc = executed VALU issue
+            # (profiles/pmc_latest.json, same config)
+            "critical_path": critical,
+            "pmc": pmc,
             "hbm": {
                 "achieved": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 3),
                 "peak": PEAK_HBM_GBS,
