@@ -39,6 +39,14 @@ PEAK_FP32_TFLOPS = 157.3
 PEAK_FP32_UNPACKED_TFLOPS = 78.6
 PEAK_HBM_GBS = 8000.0
 BLOCK_ROWS = 8
+# BASELINE.json configs: name -> (width, height, max_steps)
+WORKLOADS = {
+    "small": (640, 360, 1000),       # config 2
+    "headline": (1920, 1080, 2000),  # config 3 (the metric)
+    "4k": (3840, 2160, 4000),        # config 4
+    "8k": (7680, 4320, 8000),        # config 5 (offline still)
+}
+MODES = {"curved": 0, "flat": 1, "half_width": 2, "half_height": 3}
 
 
 def parse():
@@ -46,9 +54,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="headline",
+                    help="BASELINE.json config (width x height / steps); --width/--height/--max-steps override")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--max-steps", type=int, default=0)
+    ap.add_argument("--mode", choices=["curved", "flat", "half_width", "half_height"], default="curved",
+                    help="raytrace_type (frag:865-878); the split modes use --curved-percentage")
+    ap.add_argument("--curved-percentage", type=float, default=0.5)
+    ap.add_argument("--percent-black", type=float, default=-1.0,
+                    help="noise mask (frag:839-841, 879); the app runs 0.75, the headline -1 (off)")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
@@ -76,12 +91,14 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    W, H, N = args.width, args.height, args.max_steps
+    W0, H0, N0 = WORKLOADS[args.workload]
+    W, H, N = args.width or W0, args.height or H0, args.max_steps or N0
 
     # ---- inputs resident in HBM ---------------------------------------------------
     scene = sc.scene_default(textured=True)
     cam = abi.default_camera()
-    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    params = abi.default_params(max_steps=N, percent_black=args.percent_black, raytrace_type=MODES[args.mode],
+                                curved_percentage=args.curved_percentage)
     r = pkg.Renderer(local)
     r.set_scene(scene)
     r.set_background(sc.skybox(2048, 1024))
@@ -245,7 +262,8 @@ def main():
         if args.cpu_baseline == "auto" and world == 1:
             cpu = cpu_baseline(cam, W, H, N, args.cpu_sample_rows)
         line = {
-            "metric": "Mpixels/s at 1920x1080, 2000 geodesic steps; 1/2/4/8 MI355X",
+            "metric": ("Mpixels/s at 1920x1080, 2000 geodesic steps; 1/2/4/8 MI355X"
+                       if (W, H, N) == WORKLOADS["headline"] else f"Mpixels/s at {W}x{H}, {N} geodesic steps"),
             "value": round(mpix_s, 3),
             "unit": "Mpixels/s",
             "n_gpus": world,
@@ -258,7 +276,10 @@ def main():
             "dtype": "f32",
             "data": "synthetic (default scene of src/main.cpp:222-268, procedural stand-in textures)",
             "config": {
-                "workload": f"{W}x{H} curved-mode frame, {N} geodesic steps, default scene, percent_black off",
+                "workload": (f"{W}x{H} {args.mode}-mode frame"
+                             + (f" (curved_percentage {args.curved_percentage})" if args.mode.startswith("half") else "")
+                             + f", {N} geodesic steps, default scene, percent_black "
+                             + ("off" if args.percent_black < 0 else str(args.percent_black))),
                 "width": W,
                 "height": H,
                 "max_steps": N,
