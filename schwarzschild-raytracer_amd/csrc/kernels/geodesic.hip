@@ -1426,15 +1426,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         float un, dun, rB, Tn, lim;
         uint32_t par;
         for (;;) {
-#ifdef SR_EXP_VTABLE  // experiment: table through the vector memory path (keeps the scalar cache for scene data)
-            int vz_;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(vz_));
-            e = tp[vz_];
-            const float g = tp[vz_ + 1].x;
-#else
             e = tp[0];  // wave-uniform scalar loads
             const float g = tp[1].x;
-#endif
             rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
             rB = __builtin_amdgcn_rcpf(un);
             Tn = bs.T;
@@ -1461,9 +1454,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             r.u = un;
             r.du = dun;
             rA = rB;
-#ifndef SR_EXP_CONST_TABLE  // timing experiment only: every step reads entry 0 (wrong output)
             tp += 2;
-#endif
             if (++i >= N) break;
         }
         SR_PT(0);
