@@ -52,7 +52,7 @@ MODES = {"curved": 0, "flat": 1, "half_width": 2, "half_height": 3}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="headline",
                     help="BASELINE.json config (width x height / steps); --width/--height/--max-steps override")
@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--percent-black", type=float, default=-1.0,
                     help="noise mask (frag:839-841, 879); the app runs 0.75, the headline -1 (off)")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight per GPU, each on its own context and stream (0: min(4, N + 1))")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
@@ -99,24 +101,39 @@ def main():
     cam = abi.default_camera()
     params = abi.default_params(max_steps=N, percent_black=args.percent_black, raytrace_type=MODES[args.mode],
                                 curved_percentage=args.curved_percentage)
-    r = pkg.Renderer(local)
-    r.set_scene(scene)
-    r.set_background(sc.skybox(2048, 1024))
+    # Frames in flight: a frame's time is bounded by the latency of its
+    # longest rays' waves, which a share of 1/N of the rows
+    # does not shorten; independent frames on their own contexts and streams
+    # fill the SIMDs those waves leave idle. Step f renders frame f on context
+    # f % F and gathers it to rank 0 on that context's stream.
+    F = args.inflight if args.inflight > 0 else min(4, world + 1)
+    skybox = sc.skybox(2048, 1024)
     arr, _, _ = sc.default_texture_array()
-    r.set_texture_array(arr)
-    r.set_culling(not args.no_cull)
-
     D = pkg.dist
-    tile = torch.zeros((D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
-    gather = D.FrameGather(tile, world, rank, H, BLOCK_ROWS)
-    stream = torch.cuda.current_stream(dev)
+    ctxs = []
+    for k in range(F):
+        rk = pkg.Renderer(local)
+        rk.set_scene(scene)
+        rk.set_background(skybox)
+        rk.set_texture_array(arr)
+        rk.set_culling(not args.no_cull)
+        tile_k = torch.zeros((D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
+        ctxs.append((rk, tile_k, D.FrameGather(tile_k, world, rank, H, BLOCK_ROWS),
+                     torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)))
+    r, tile, gather, stream = ctxs[0]
 
     def render_tile():
         r.render_blocks(cam, params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
 
-    def step():
-        render_tile()
-        return gather()  # the assembled frame on rank 0 (RCCL gather for N > 1)
+    def step(f=0):
+        rk, tile_k, gather_k, s_k = ctxs[f % F]
+        with torch.cuda.stream(s_k):
+            rk.render_blocks(cam, params, W, H, BLOCK_ROWS, rank, world, out=tile_k, stream=s_k)
+            return gather_k()  # the assembled frame on rank 0 (RCCL gather for N > 1)
+
+    def sync_all():
+        for _, _, _, s_k in ctxs:
+            s_k.synchronize()
 
     # executed steps of this rank's rows (untimed; the debug variant of the kernel)
     rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
@@ -128,9 +145,9 @@ def main():
     band_row = int(steps_full.max(dim=1).values.argmax().item()) // 16 * 16
     del steps_full
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
+    for f in range(max(args.warmup, F)):  # every context learns its launch order
+        step(f)
+    sync_all()
 
     # kernel-only timing with HIP events on the render stream (separate loop
     # so the gather does not sit between the events); the library records
@@ -149,10 +166,12 @@ def main():
 
     if distributed:
         dist.barrier()
+    sync_all()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for f in range(args.steps):
+        step(f)
+    sync_all()
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
@@ -178,7 +197,7 @@ def main():
     if rank == 0 and world == 1:
         rb = pkg.Renderer(local)
         rb.set_scene(scene)
-        rb.set_background(sc.skybox(2048, 1024))
+        rb.set_background(skybox)
         rb.set_texture_array(arr)
         rb.set_culling(not args.no_cull)
         band = (band_row, min(H, band_row + 16))
@@ -284,6 +303,8 @@ def main():
                 "height": H,
                 "max_steps": N,
                 "tiling": f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), RCCL gather to rank 0",
+                "frames_in_flight": F,
+                "frame_latency_ms": round(kernel_ms_max, 4),
                 "culling": not args.no_cull,
                 "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
             },
@@ -294,7 +315,8 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
-    r.close()
+    for rk, _, _, _ in ctxs:
+        rk.close()
 
 
 def cpu_baseline(cam, W, H, N, sample_rows):

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Frames in flight on one GPU: F contexts, each on its own stream, render K
+frames of the headline frame round-robin; prints frames/s and Mpix/s per F.
+The frame's time is bounded by its longest rays' waves; with
+several frames in flight the next frames' waves fill the SIMDs those leave idle.
+  python tools/inflight.py [--frames 24] [--inflight 1 2 3 4]"""
+import argparse
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=24)
+    ap.add_argument("--inflight", type=int, nargs="+", default=[1, 2, 3, 4])
+    args = ap.parse_args()
+    import torch
+
+    import srpkg
+
+    pkg = srpkg.load_package()
+    abi, sc = pkg.abi, pkg.scenes
+    scene = sc.scene_default(textured=True)
+    bg = sc.skybox(2048, 1024)
+    arr, _, _ = sc.default_texture_array()
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+    W, H = 1920, 1080
+    rs, ss, outs = [], [], []
+    for k in range(max(args.inflight)):
+        r = pkg.Renderer(0)
+        r.set_scene(scene)
+        r.set_background(bg)
+        r.set_texture_array(arr)
+        rs.append(r)
+        ss.append(torch.cuda.Stream())
+        outs.append(torch.empty((H, W, 4), dtype=torch.uint8, device="cuda"))
+    for k in range(len(rs)):  # learn each context's launch order
+        for _ in range(2):
+            rs[k].render(cam, params, W, H, out=outs[k], stream=ss[k])
+    torch.cuda.synchronize()
+    for F in args.inflight:
+        t0 = time.perf_counter()
+        for f in range(args.frames):
+            k = f % F
+            rs[k].render(cam, params, W, H, out=outs[k], stream=ss[k])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        print(f"in flight {F}: {dt * 1e3 / args.frames:.4f} ms/frame, {W * H * args.frames / dt / 1e6:.1f} Mpix/s", flush=True)
+    for r in rs:
+        r.close()
+
+
+if __name__ == "__main__":
+    main()
