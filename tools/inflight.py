@@ -17,6 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--inflight", type=int, nargs="+", default=[1, 2, 3, 4])
+    ap.add_argument("--shard", type=int, nargs=2, default=[0, 1], metavar=("RANK", "N"),
+                    help="render only this rank's block-cyclic share of an N-GPU frame (8-row blocks)")
     args = ap.parse_args()
     import torch
 
@@ -30,6 +32,8 @@ def main():
     cam = abi.default_camera()
     params = abi.default_params(max_steps=2000, percent_black=-1.0)
     W, H = 1920, 1080
+    rank, world = args.shard
+    D = pkg.dist
     rs, ss, outs = [], [], []
     for k in range(max(args.inflight)):
         r = pkg.Renderer(0)
@@ -38,19 +42,20 @@ def main():
         r.set_texture_array(arr)
         rs.append(r)
         ss.append(torch.cuda.Stream())
-        outs.append(torch.empty((H, W, 4), dtype=torch.uint8, device="cuda"))
+        outs.append(torch.empty((D.tile_rows(world, H, 8), W, 4), dtype=torch.uint8, device="cuda"))
     for k in range(len(rs)):  # learn each context's launch order
         for _ in range(2):
-            rs[k].render(cam, params, W, H, out=outs[k], stream=ss[k])
+            rs[k].render_blocks(cam, params, W, H, 8, rank, world, out=outs[k], stream=ss[k])
     torch.cuda.synchronize()
     for F in args.inflight:
         t0 = time.perf_counter()
         for f in range(args.frames):
             k = f % F
-            rs[k].render(cam, params, W, H, out=outs[k], stream=ss[k])
+            rs[k].render_blocks(cam, params, W, H, 8, rank, world, out=outs[k], stream=ss[k])
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-        print(f"in flight {F}: {dt * 1e3 / args.frames:.4f} ms/frame, {W * H * args.frames / dt / 1e6:.1f} Mpix/s", flush=True)
+        print(f"shard {rank}/{world}, in flight {F}: {dt * 1e3 / args.frames:.4f} ms/frame "
+              f"({W * H * args.frames / dt / 1e6:.1f} whole-frame Mpix/s if every rank kept this pace)", flush=True)
     for r in rs:
         r.close()
 
