@@ -210,6 +210,54 @@ def test_headline_frame_sampled_rows(pkg, gpu, oracle, oracle_tex):
     assert 380 < s.mean() < 440, s.mean()
 
 
+def test_config4_rank_share_4k(pkg, gpu, oracle, oracle_tex):
+    """BASELINE config 4 (3840x2160, 4000 steps, row-tiled over 8 GPUs): rank
+    3's block-cyclic share rendered through sr_render_blocks, the multi-GPU
+    data path of bench.py, and three of its rows bit-compared with the oracle."""
+    import torch
+
+    sc, abi, D = pkg.scenes, pkg.abi, pkg.dist
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=4000, percent_black=-1.0)
+    W, H, br, world, rank = 3840, 2160, 8, 8, 3
+    gpu.set_scene(scene)
+    gpu.set_test_ray(abi.default_test_ray())
+    tile, nrows = gpu.render_blocks(cam, params, W, H, br, rank, world)
+    torch.cuda.synchronize()
+    tile = tile.cpu().numpy()
+    rows = D.rows_of(rank, world, H, br)
+    assert nrows == len(rows) and tile.shape[0] >= len(rows)
+    for k in (0, len(rows) // 2 + 3, len(rows) - 1):  # edge, through the photon ring, edge
+        y = rows[k]
+        rb, _, _ = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
+        assert (rb[0] != tile[k]).any(-1).mean() <= 1e-3, f"row {y}"
+
+
+def test_config5_band_8k(pkg, gpu, oracle, oracle_tex):
+    """BASELINE config 5 (7680x4320 offline still, 8000 steps): a 16-row band
+    through the black hole rendered alone, two rows bit-compared with the
+    oracle (executed step counts too)."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=8000, percent_black=-1.0)
+    W, H = 7680, 4320
+    y0 = H // 2 - 8
+    gpu.set_scene(scene)
+    gpu.set_test_ray(abi.default_test_ray())
+    _, b, s = gpu.render_debug(cam, params, W, H, y0, y0 + 16)
+    torch.cuda.synchronize()
+    b, s = b.cpu().numpy(), s.cpu().numpy()
+    for k in (3, 12):
+        y = y0 + k
+        rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, y, y + 1)
+        assert (rb[0] != b[k]).any(-1).mean() <= 1e-3, f"row {y}"
+        assert (rs[0] != s[k]).mean() <= 1e-3, f"row {y}"
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_random_scenes(pkg, gpu, oracle, oracle_tex, seed):
     """Stress scenes: 18-21 objects - more than the

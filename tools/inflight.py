@@ -17,9 +17,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--inflight", type=int, nargs="+", default=[1, 2, 3, 4])
+    ap.add_argument("--lib", default="", help="libsr variant to load (default: the package's)")
     ap.add_argument("--shard", type=int, nargs=2, default=[0, 1], metavar=("RANK", "N"),
                     help="render only this rank's block-cyclic share of an N-GPU frame (8-row blocks)")
     args = ap.parse_args()
+    if args.lib:
+        import os
+
+        os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch
 
     import srpkg
