@@ -1,0 +1,54 @@
+"""bench.py's command line (driver contract) and its workloads against
+BASELINE.json's configs; no GPU needed."""
+import json
+import re
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _parse(argv):
+    import bench
+
+    old = sys.argv
+    sys.argv = ["bench.py"] + argv
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+def test_defaults_are_the_headline_on_one_gpu():
+    import bench
+
+    a = _parse([])
+    assert a.gpus == 1 and a.workload == "headline" and a.mode == "curved" and a.percent_black < 0
+    assert bench.WORKLOADS["headline"] == (1920, 1080, 2000)
+    assert a.steps >= 1 and a.warmup >= 0 and a.inflight == 0
+
+
+def test_driver_flags_parse():
+    a = _parse(["--gpus", "8", "--steps", "5", "--warmup", "2"])
+    assert (a.gpus, a.steps, a.warmup) == (8, 5, 2)
+
+
+def test_workloads_match_baseline_configs():
+    import bench
+
+    configs = json.loads((ROOT / "BASELINE.json").read_text())["configs"]
+    sizes = []
+    for c in configs:
+        m = re.search(r"(\d+)x(\d+)[^,]*, (\d+) steps", c)
+        if m:
+            sizes.append(tuple(int(v) for v in m.groups()))
+    assert sorted(sizes) == sorted(bench.WORKLOADS.values())
+    metric = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+    assert "1920x1080" in metric and "2000" in metric
+
+
+def test_help_runs_without_a_gpu():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "--workload" in r.stdout and "--inflight" in r.stdout
