@@ -1268,16 +1268,21 @@ __device__ __forceinline__ float point_err(float rA, float rB) { return 4.0e-6f 
 __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 
 // rk4_step, frag:341-355, plus the `u += .x; du += .y` of frag:918-919 (h6 =
-// `delta_phi / 6.`, computed on the host). The u and u' halves of each stage
-// are the same operations on different operands, so they run as packed
-// binary32 pairs (v_pk_mul_f32 / v_pk_add_f32: two correctly rounded results
-// per lane, bit-identical to the scalar expressions):
-//   (ua, k2) = (u, u') + (0.5 (k1, l1)) h      l2 = ddu(ua)
-//   (ub, k3) = (u, u') + (0.5 (k2, l2)) h      l3 = ddu(ub)
+// `delta_phi / 6.` and hh = 0.5 h, computed on the host). The u and u' halves
+// of each stage are the same operations on different operands, so they run
+// as packed binary32 pairs (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two
+// correctly rounded results per lane):
+//   (ua, k2) = (u, u') + (k1, l1) hh           l2 = ddu(ua)
+//   (ub, k3) = (u, u') + (k2, l2) hh           l3 = ddu(ub)
 //   (uc, k4) = (u, u') + (k3, l3) h            l4 = ddu(uc)
-//   (u, u') += h6 (((k1, l1) + 2 (k2, l2)) + 2 (k3, l3)) + (k4, l4))
+//   (u, u') += h6 ((fma(2, (k3, l3), fma(2, (k2, l2), (k1, l1)))) + (k4, l4))
+// Bit-identical to the reference's expressions: (0.5 q) h and q (0.5 h) are
+// both the rounding of the same product, as scaling by 0.5 is exact for
+// non-subnormal q (the stage values here are never subnormal: DESIGN.md §4);
+// and 2 q is exact, so fma(2, q, a) is the rounding of a + 2 q, as the
+// reference's a + (2. * q).
 typedef float v2f __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void rk4_step(float u, float du, float h, float h6, float& un, float& dun) {
+__device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, float h6, float& un, float& dun) {
 #ifdef SR_SCALAR_RK4
     const float k1 = du;
     const float l1 = ddu(u);
@@ -1291,16 +1296,16 @@ __device__ __forceinline__ void rk4_step(float u, float du, float h, float h6, f
     dun = du + h6 * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
 #else
     const v2f s0 = {u, du};
-    const v2f hh = {h, h};
+    const v2f H1 = {h, h}, H2 = {hh, hh}, two = {2.0f, 2.0f};
     const v2f q1 = {du, ddu(u)};
-    const v2f p1 = s0 + (0.5f * q1) * hh;
+    const v2f p1 = s0 + q1 * H2;
     const v2f q2 = {p1.y, ddu(p1.x)};
-    const v2f p2 = s0 + (0.5f * q2) * hh;
+    const v2f p2 = s0 + q2 * H2;
     const v2f q3 = {p2.y, ddu(p2.x)};
-    const v2f p3 = s0 + q3 * hh;
+    const v2f p3 = s0 + q3 * H1;
     const v2f q4 = {p3.y, ddu(p3.x)};
     const v2f hs = {h6, h6};
-    const v2f r = s0 + hs * (((q1 + 2.0f * q2) + 2.0f * q3) + q4);
+    const v2f r = s0 + hs * (__builtin_elementwise_fma(two, q3, __builtin_elementwise_fma(two, q2, q1)) + q4);
     un = r.x;
     dun = r.y;
 #endif
@@ -1427,18 +1432,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         uint32_t par;
         for (;;) {
             e = tp[0];  // wave-uniform scalar loads
-            const float g = tp[1].x;
-            rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
+            const float4 e1 = tp[1];  // {g, 0.5 step_size, K_i, -}
+            rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
             rB = __builtin_amdgcn_rcpf(un);
             Tn = bs.T;
             lim = lim0;
             par = 0;
             if (CULL) {
-                // chord length bound: sqrt(dr^2 + rA rB g) (1 + 1e-4) + point_err, times the
-                // path slack (bounds, not reference arithmetic: FMA allowed)
+                // chord length bound: sqrt(dr^2 + rA rB g) K_i, K_i covering the 1e-4
+                // relative allowance, point_err (<= 4e-6 (2 / sqrt(g) + 1) sqrt(...):
+                // sr_api.cpp ensure_table) and the path slack (bounds, not reference
+                // arithmetic: FMA allowed)
                 const float dr = rB - rA;
-                const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * g));
-                Tn = __builtin_fmaf(rA + rB, 4.0e-6f * SR_PATH_SLACK, __builtin_fmaf(sq, 1.0001f * SR_PATH_SLACK, Tn));
+                const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
+                Tn = __builtin_fmaf(sq, e1.z, Tn);
                 if (any_cm) {
                     const f2 p1 = phi_cs(i - 1);
                     par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));

@@ -282,7 +282,12 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
     // vectors (cos, sin) of steps i - 1 and i (n = squared norm, p = their dot;
     // step -1 is phi = 0): the squared chord of two orbit points at radii
     // r1, r2 is (r2 - r1)^2 + r1 r2 g up to float rounding (kernel chord
-    // bound). One padding entry.
+    // bound). The second float4 is {g, 0.5 step_size, K, 0}: 0.5 step_size for
+    // RK4 (exact), and K the chord bound's factor: a chord's float end points
+    // lie within 4e-6 (r1 + r2) of the ideal ones, and r1 + r2 <= (2 / sqrt(g)
+    // + 1) sqrt((r2 - r1)^2 + r1 r2 g) (min(r1, r2) <= sqrt(r1 r2)), so
+    // K = (1.0001 + 4.01e-6 (2.001 / sqrt(g) + 1)) x path slack 1.01, rounded
+    // up, covers both. One padding entry.
     std::vector<float4> h(2 * ((size_t)max_steps + 1), make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
     double c1 = 1.0, s1 = 0.0;
@@ -294,7 +299,8 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
         const double n1 = c1 * c1 + s1 * s1, n2 = (double)c * c + (double)sn * sn, pr = c1 * c + s1 * sn;
         double g = 2.0 * (std::sqrt(n1 * n2) - pr);
         g = g > 0.0 ? g * (1.0 + 1e-6) + 1e-30 : 1e-30;  // rounded up
-        h[2 * (size_t)i + 1] = make_float4((float)g, 0.f, 0.f, 0.f);
+        const double K = (1.0001 + 4.01e-6 * (2.001 / std::sqrt(g) + 1.0)) * 1.01 * (1.0 + 1e-6);
+        h[2 * (size_t)i + 1] = make_float4((float)g, 0.5f * step, std::nextafter((float)K, INFINITY), 0.f);
         c1 = c;
         s1 = sn;
     }
