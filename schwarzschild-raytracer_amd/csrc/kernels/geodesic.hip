@@ -13,6 +13,8 @@
 // transcendentals rounded to binary32, GLSL evaluation order.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../device_scene.h"
 
 namespace {
@@ -1295,17 +1297,20 @@ __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, f
     un = u + h6 * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
     dun = du + h6 * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
 #else
+    // Each stage's (u_stage, k) pair is overwritten in place by (l, k) =
+    // (ddu(u_stage), k); the next stage reads it swapped (op_sel), so no
+    // pair is ever assembled with register moves.
     const v2f s0 = {u, du};
     const v2f H1 = {h, h}, H2 = {hh, hh}, two = {2.0f, 2.0f};
     const v2f q1 = {du, ddu(u)};
-    const v2f p1 = s0 + q1 * H2;
-    const v2f q2 = {p1.y, ddu(p1.x)};
-    const v2f p2 = s0 + q2 * H2;
-    const v2f q3 = {p2.y, ddu(p2.x)};
-    const v2f p3 = s0 + q3 * H1;
-    const v2f q4 = {p3.y, ddu(p3.x)};
+    v2f p1 = s0 + q1 * H2;  // (ua, k2)
+    p1.x = ddu(p1.x);       // (l2, k2)
+    v2f p2 = s0 + p1.yx * H2;  // (ub, k3)
+    p2.x = ddu(p2.x);          // (l3, k3)
+    v2f p3 = s0 + p2.yx * H1;  // (uc, k4)
+    p3.x = ddu(p3.x);          // (l4, k4)
     const v2f hs = {h6, h6};
-    const v2f r = s0 + hs * (__builtin_elementwise_fma(two, q3, __builtin_elementwise_fma(two, q2, q1)) + q4);
+    const v2f r = s0 + hs * (__builtin_elementwise_fma(two, p2.yx, __builtin_elementwise_fma(two, p1.yx, q1)) + p3.yx);
     un = r.x;
     dun = r.y;
 #endif
@@ -1430,40 +1435,48 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         float4 e;
         float un, dun, rB, Tn, lim;
         uint32_t par;
-        for (;;) {
-            e = tp[0];  // wave-uniform scalar loads
-            const float4 e1 = tp[1];  // {g, 0.5 step_size, K_i, -}
-            rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
-            rB = __builtin_amdgcn_rcpf(un);
-            Tn = bs.T;
+        // Two versions of the loop: without a lane whose orbital plane nearly
+        // contains a budgeted cylinder's axis (the usual case) the limit is
+        // fixed and there is no direction test.
+        auto fast = [&](auto cm_tag) {
+            constexpr bool CM = decltype(cm_tag)::value;
             lim = lim0;
             par = 0;
-            if (CULL) {
-                // chord length bound: sqrt(dr^2 + rA rB g) K_i, K_i covering the 1e-4
-                // relative allowance, point_err (<= 4e-6 (2 / sqrt(g) + 1) sqrt(...):
-                // sr_api.cpp ensure_table) and the path slack (bounds, not reference
-                // arithmetic: FMA allowed)
-                const float dr = rB - rA;
-                const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
-                Tn = __builtin_fmaf(sq, e1.z, Tn);
-                if (any_cm) {
-                    const f2 p1 = phi_cs(i - 1);
-                    par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));
-                    if (par) lim = nmin(lim, bs.mh);
+            for (;;) {
+                e = tp[0];  // wave-uniform scalar loads
+                const float4 e1 = tp[1];  // {g, 0.5 step_size, K_i, -}
+                rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
+                rB = __builtin_amdgcn_rcpf(un);
+                Tn = bs.T;
+                if (CULL) {
+                    // chord length bound: sqrt(dr^2 + rA rB g) K_i, K_i covering the 1e-4
+                    // relative allowance, point_err (<= 4e-6 (2 / sqrt(g) + 1) sqrt(...):
+                    // sr_api.cpp ensure_table) and the path slack (bounds, not reference
+                    // arithmetic: FMA allowed)
+                    const float dr = rB - rA;
+                    const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
+                    Tn = __builtin_fmaf(sq, e1.z, Tn);
+                    if (CM) {
+                        const f2 p1 = phi_cs(i - 1);
+                        par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));
+                        lim = par ? nmin(lim0, bs.mh) : lim0;
+                    }
                 }
+                SR_STAT(0, 1);
+                SR_STAT(13, __popcll(__ballot(1)));
+                // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
+                if (__ballot(!(Tn < lim) || un < fr.u_f)) break;
+                bs.T = Tn;
+                up = r.u;
+                r.u = un;
+                r.du = dun;
+                rA = rB;
+                tp += 2;
+                if (++i >= N) break;
             }
-            SR_STAT(0, 1);
-            SR_STAT(13, __popcll(__ballot(1)));
-            // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
-            if (__ballot(!(Tn < lim) || un < fr.u_f)) break;
-            bs.T = Tn;
-            up = r.u;
-            r.u = un;
-            r.du = dun;
-            rA = rB;
-            tp += 2;
-            if (++i >= N) break;
-        }
+        };
+        if (any_cm) fast(std::true_type{});
+        else fast(std::false_type{});
         SR_PT(0);
         if (i >= N) break;
         // ---- slow path of step i
