@@ -75,6 +75,24 @@ typedef struct {
     float f[SR_OBJ_FLOATS - 4];
 } sr_dev_obj;  // 512 B
 
+// A budget slot's object in the compact form the budget events read (slot j
+// >= 1 is slots[j - 1]): one scalar-load batch instead of chains through
+// budget_idx and the 512 B record. Extents x0..x2 by type:
+//   rectangle: width, height, -      box: width, depth, height
+//   disk: radius, -, -               hollow disk: inner, outer radius, -
+//   cylinder: height, radius, -      sphere: -
+typedef struct {
+    int32_t type;
+    int32_t cyl;     // k among the budgeted cylinders (budget_cyl_mask bit order), -1 otherwise
+    float rb, mp, br, mu, pl1;  // as in sr_dev_obj
+    float qk;        // cylinders: SR_CYL_QMARGIN / (radius SR_BUDGET_DPMIN), rounded away from zero
+    float bc[3], x0;
+    float pos[3], x1;
+    float a0[3], x2;  // axes[0..2] (columns)
+    float a1[3], pad0;
+    float a2[3], pad1;
+} sr_dev_slot;  // 128 B
+
 // Per-pixel state planes passed between the integrate / shade / resume kernels
 // (geodesic.hip PS_*): status, step, steps, hit count, frag[4], ro, rd, nv, tv,
 // u, du, then SR_PS_HITS hit records {p[3], slot * 8 + face, chord dir[3], steps}.
@@ -96,6 +114,7 @@ typedef struct {
     int32_t num_budget;       // objects of SR_KIND_BUDGET (<= SR_MAX_BUDGET)
     int32_t budget_idx[SR_MAX_OBJECTS];  // their indices in objs[]
     int32_t budget_cyl_mask;  // bit j-1 set: budget slot j is a cylinder
+    sr_dev_slot slots[SR_MAX_BUDGET];  // budget slots 1..num_budget
     int32_t num_step;         // objects of SR_KIND_EXACT / SR_KIND_CHORD (tested every step)
     int32_t step_idx[SR_MAX_OBJECTS];
     float tr_curved_color[4];

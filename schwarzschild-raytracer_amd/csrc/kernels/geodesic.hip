@@ -109,7 +109,10 @@ __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
 // so the build keeps the production register allocation as far as possible).
 //   0 fast loop  1 reseeds  2 slow-path entry + approximate chord  3 budget events phase 1
 //   4 exact chord + intersect  5 hit classification + log  6 budget events phase 2  7 wave total
-#define SR_PROF_N 16  // 0-6 sections, 7 wave total | max steps << 48, 8-15 re-anchors of budget slots 0-7
+#define SR_PROF_N 24  // 0-6 sections, 7 wave total | max steps << 48, 8-15 re-anchors of budget slots 0-7,
+                      // 16 budget events, 17 events spending only slot 0, 18 lanes spending slot 0 (sum),
+                      // 19 slow-path entries, 20 event phase 1 up to the spent ballots (the rest
+                      // in 3), 21 slow-path tail + top of the step loop (2: exit to the event)
 __device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
 #define SR_PT(k)                                                      \
     do {                                                              \
@@ -328,52 +331,89 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // direction are tested per chord instead (budget_parallel). Computed with
 // hardware sqrt: its error is far below the margins.
 #define SR_PATH_SLACK 1.01f
-__device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
+__device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, float a) {
     float c;
-    if (j == 0) {
-        // black hole: sphere_test accepts only its entry or exit point, on the
-        // r = 1 shell (a ray can cross the shell between steps and go on inside)
-        c = fabsf(a - 1.0f) - SR_MU_QUADRATIC * 3.0f;
-    } else {
-        const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
-        f3 w = A - ld3(ob.bc);
-        c = __builtin_amdgcn_sqrtf(dot(w, w)) - ob.rb;
-        if (ob.mp < INFINITY) {  // distance to the primitive itself (orthonormal frame)
-            const float* f = ob.f;
-            const f3 q = A - ld3(f + SR_F_POS);
-            const float y = dot(q, ld3(f + SR_F_AXES + 3));  // along axes[1] (plane normal / height)
+    {
+        f3 w = A - ld3(sl.bc);
+        c = __builtin_amdgcn_sqrtf(dot(w, w)) - sl.rb;
+        if (sl.mp < INFINITY) {  // distance to the primitive itself (orthonormal frame)
+            const f3 q = A - ld3(sl.pos);
+            const float y = dot(q, ld3(sl.a1));  // along axes[1] (plane normal / height)
             float d2;
-            if (ob.type == SR_OBJECT_PLANE) {
+            if (sl.type == SR_OBJECT_PLANE) {
                 d2 = y * y;
-            } else if (ob.type == SR_OBJECT_RECTANGLE || ob.type == SR_OBJECT_BOX) {
-                const float x = dot(q, ld3(f + SR_F_AXES)), z = dot(q, ld3(f + SR_F_AXES + 6));
-                const bool box = ob.type == SR_OBJECT_BOX;
-                const float wx = box ? f[12] : f[17], wz = box ? f[13] : f[18];
-                const float ex = fmaxf(0.0f, fmaxf(-x, x - wx)), ez = fmaxf(0.0f, fmaxf(-z, z - wz));
-                const float ey = box ? fmaxf(0.0f, fmaxf(-y, y - f[14])) : y;
+            } else if (sl.type == SR_OBJECT_RECTANGLE || sl.type == SR_OBJECT_BOX) {
+                const float x = dot(q, ld3(sl.a0)), z = dot(q, ld3(sl.a2));
+                const bool box = sl.type == SR_OBJECT_BOX;
+                const float ex = fmaxf(0.0f, fmaxf(-x, x - sl.x0)), ez = fmaxf(0.0f, fmaxf(-z, z - sl.x1));
+                const float ey = box ? fmaxf(0.0f, fmaxf(-y, y - sl.x2)) : y;
                 d2 = ex * ex + ey * ey + ez * ez;
             } else {  // disk, hollow disk, cylinder: radial distance from axes[1]
                 const float rho = __builtin_amdgcn_sqrtf(fmaxf(0.0f, dot(q, q) - y * y));
                 float er, ey = y;
-                if (ob.type == SR_OBJECT_DISK) {
-                    er = fmaxf(0.0f, rho - f[17]);
-                } else if (ob.type == SR_OBJECT_HOLLOW_DISK) {
-                    er = fmaxf(0.0f, fmaxf(f[17] - rho, rho - f[18]));
+                if (sl.type == SR_OBJECT_DISK) {
+                    er = fmaxf(0.0f, rho - sl.x0);
+                } else if (sl.type == SR_OBJECT_HOLLOW_DISK) {
+                    er = fmaxf(0.0f, fmaxf(sl.x0 - rho, rho - sl.x1));
                 } else {
-                    er = fmaxf(0.0f, rho - f[SR_F_P0 + 1]);
-                    ey = fmaxf(0.0f, fmaxf(-y, y - f[SR_F_P0]));
+                    er = fmaxf(0.0f, rho - sl.x1);
+                    ey = fmaxf(0.0f, fmaxf(-y, y - sl.x0));
                 }
                 d2 = er * er + ey * ey;
             }
-            c = fmaxf(c, __builtin_amdgcn_sqrtf(d2) - ob.mp);
+            c = fmaxf(c, __builtin_amdgcn_sqrtf(d2) - sl.mp);
         }
-        if (ob.type == SR_OBJECT_CYLINDER) {
-            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + ob.pl1 + (3.0f * SR_BUDGET_TMAX + 1.0f);
-            float qm = SR_CYL_QMARGIN * Sb * Sb / (ob.f[SR_F_P0 + 1] * SR_BUDGET_DPMIN);
+        if (sl.type == SR_OBJECT_CYLINDER) {
+            // quadratic margin SR_CYL_QMARGIN Sb^2 / (r SR_BUDGET_DPMIN), the
+            // quotient folded into sl.qk on the host
+            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + (3.0f * SR_BUDGET_TMAX + 1.0f);
+            float qm = (Sb * Sb) * sl.qk;
             c = fminf(c - qm, SR_BUDGET_TMAX);
         }
     }
     return c - 1.8f * SR_MU_QUADRATIC * a;
+}
+// black hole: sphere_test accepts only its entry or exit point, on the r = 1
+// shell (a ray can cross the shell between steps and go on inside)
+__device__ __forceinline__ float clearance_bh(float a) {
+    return (fabsf(a - 1.0f) - SR_MU_QUADRATIC * 3.0f) - 1.8f * SR_MU_QUADRATIC * a;
+}
+__device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
+    return j == 0 ? clearance_bh(a) : clearance_obj(sc->slots[j - 1], A, a);
+}
+
+// A budget slot's record read in one batch of scalar loads: every field is
+// pinned to an SGPR where it is loaded, so the type-specific code that
+// follows does not wait on a chain of lazily issued loads.
+#define SR_PIN(x) asm volatile("" : "+s"(x))
+__device__ __forceinline__ sr_dev_slot pin_slot(const sr_dev_slot& g) {
+    sr_dev_slot sl = g;
+    SR_PIN(sl.type);
+    SR_PIN(sl.rb);
+    SR_PIN(sl.mp);
+    SR_PIN(sl.br);
+    SR_PIN(sl.mu);
+    SR_PIN(sl.pl1);
+    SR_PIN(sl.qk);
+    SR_PIN(sl.bc[0]);
+    SR_PIN(sl.bc[1]);
+    SR_PIN(sl.bc[2]);
+    SR_PIN(sl.x0);
+    SR_PIN(sl.pos[0]);
+    SR_PIN(sl.pos[1]);
+    SR_PIN(sl.pos[2]);
+    SR_PIN(sl.x1);
+    SR_PIN(sl.a0[0]);
+    SR_PIN(sl.a0[1]);
+    SR_PIN(sl.a0[2]);
+    SR_PIN(sl.x2);
+    SR_PIN(sl.a1[0]);
+    SR_PIN(sl.a1[1]);
+    SR_PIN(sl.a1[2]);
+    SR_PIN(sl.a2[0]);
+    SR_PIN(sl.a2[1]);
+    SR_PIN(sl.a2[2]);
+    return sl;
 }
 
 // Direction-independent part of a budgeted cylinder's clearance: the distance
@@ -382,11 +422,11 @@ __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, 
 // chord up to rounding, whose computed height passes that window, so this
 // bound holds however ill-conditioned the lateral quadratic is (chords nearly
 // parallel to the axis). Same margins as clearance(); -inf without a unit axis.
-__device__ __forceinline__ float clearance_slab(const sr_dev_obj& ob, f3 A, float a) {
-    if (!(ob.mp < INFINITY)) return -INFINITY;
-    const float y = dot(A - ld3(ob.f + SR_F_POS), ld3(ob.f + SR_F_AXES + 3));
-    const float ey = fmaxf(0.0f, fmaxf(-y, y - ob.f[SR_F_P0]));
-    return ey - ob.mp - 1.8f * SR_MU_QUADRATIC * a;
+__device__ __forceinline__ float clearance_slab(const sr_dev_slot& sl, f3 A, float a) {
+    if (!(sl.mp < INFINITY)) return -INFINITY;
+    const float y = dot(A - ld3(sl.pos), ld3(sl.a1));
+    const float ey = fmaxf(0.0f, fmaxf(-y, y - sl.x0));
+    return ey - sl.mp - 1.8f * SR_MU_QUADRATIC * a;
 }
 
 // NaN-propagating minimum: a NaN clearance must force the exact tests.
@@ -432,7 +472,7 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
-            const f3 ax = ld3(sc->objs[sc->budget_idx[__builtin_ctz(c)]].f + SR_F_AXES + 3);
+            const f3 ax = ld3(sc->slots[__builtin_ctz(c)].a1);
             const float pa = dot(nv, ax), pb = dot(tv, ax);
             bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE] = pa;
             bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
@@ -461,7 +501,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
-            const float e = clearance_slab(sc->objs[sc->budget_idx[__builtin_ctz(c)]], A, a);
+            const float e = clearance_slab(sc->slots[__builtin_ctz(c)], A, a);
             bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = e;
             mh = nmin(mh, e);
             c &= c - 1;
@@ -498,7 +538,7 @@ __device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restric
 
 // Conservative: may the exact chord, within perr of the segment [A, B], come
 // within reach of slot j's exact test (per-chord margins of may_hit)?
-__device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ sc, int j, f3 A, f3 B, float perr) {
+__device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3 A, f3 B, float perr) {
     const f3 dv = B - A;
     const float dd = dot(dv, dv);
     const float len = __builtin_amdgcn_sqrtf(dd);
@@ -513,21 +553,21 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
         const float ri = (1.0f - SR_MU_QUADRATIC * S) * 0.999f - perr;
         if (dot(A, A) < ri * ri && dot(B, B) < ri * ri && ri > 0.0f) return false;
     } else {
-        const sr_dev_obj& ob = sc->objs[sc->budget_idx[j - 1]];
-        c = ld3(ob.bc);
-        R = ob.br + ob.mu * S;
-        if (ob.mp < INFINITY) {  // orthonormal frame: tighter regions than the bounding sphere
-            const float m = (ob.mp + SR_MU_QUADRATIC * S) * 1.001f + perr;
-            const f3 pos = ld3(ob.f + SR_F_POS);
-            const f3 a1 = ld3(ob.f + SR_F_AXES + 3);
+        const sr_dev_slot& sl = *slp;
+        c = ld3(sl.bc);
+        R = sl.br + sl.mu * S;
+        if (sl.mp < INFINITY) {  // orthonormal frame: tighter regions than the bounding sphere
+            const float m = (sl.mp + SR_MU_QUADRATIC * S) * 1.001f + perr;
+            const f3 pos = ld3(sl.pos);
+            const f3 a1 = ld3(sl.a1);
             const float yA = dot(A - pos, a1), yB = dot(B - pos, a1);
-            if (ob.type == SR_OBJECT_PLANE || ob.type == SR_OBJECT_DISK || ob.type == SR_OBJECT_HOLLOW_DISK ||
-                ob.type == SR_OBJECT_RECTANGLE) {
+            if (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_DISK || sl.type == SR_OBJECT_HOLLOW_DISK ||
+                sl.type == SR_OBJECT_RECTANGLE) {
                 // planar: the chord must reach the plane's acceptance slab
                 if ((yA > m && yB > m) || (yA < -m && yB < -m)) return false;
-            } else if (ob.type == SR_OBJECT_BOX) {
+            } else if (sl.type == SR_OBJECT_BOX) {
                 // the chord must reach the box grown by the margin (slab test in the box frame)
-                const f3 a0 = ld3(ob.f + SR_F_AXES), a2 = ld3(ob.f + SR_F_AXES + 6);
+                const f3 a0 = ld3(sl.a0), a2 = ld3(sl.a2);
                 const float xA = dot(A - pos, a0), xB = dot(B - pos, a0);
                 const float zA = dot(A - pos, a2), zB = dot(B - pos, a2);
                 float t0 = 0.0f, t1 = 1.0f;
@@ -547,22 +587,22 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_scene* __restrict__ 
                     t0 = fmaxf(t0, ta);
                     t1 = fminf(t1, tb);
                 };
-                slab(xA, xB, ob.f[12]);
-                slab(yA, yB, ob.f[14]);
-                slab(zA, zB, ob.f[13]);
+                slab(xA, xB, sl.x0);
+                slab(yA, yB, sl.x2);
+                slab(zA, zB, sl.x1);
                 if (t0 > t1 + 1e-6f) return false;
-            } else if (ob.type == SR_OBJECT_CYLINDER) {
+            } else if (sl.type == SR_OBJECT_CYLINDER) {
                 // the chord must reach the height slab (clearance_slab), in any direction
-                const float hc = ob.f[SR_F_P0];
+                const float hc = sl.x0;
                 if ((yA < -m && yB < -m) || (yA > hc + m && yB > hc + m)) return false;
             }
         }
-        if (ob.type == SR_OBJECT_CYLINDER) {
-            const float ca = dot(dv, ld3(ob.f + SR_F_AXES + 3));
+        if (sl.type == SR_OBJECT_CYLINDER) {
+            const float ca = dot(dv, ld3(sl.a1));
             const float dp = (dd - ca * ca) * __builtin_amdgcn_rcpf(dd) * 0.5f;
-            const float r = ob.f[SR_F_P0 + 1];
+            const float r = sl.x1;
             if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
-            const float Sc = S + ob.pl1;
+            const float Sc = S + sl.pl1;
             R = R + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp);
         }
     }
@@ -616,6 +656,17 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     for (int j = 0; j < NS; j++)
         if (__ballot(!(T < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
     spent &= (2u << nb) - 1u;
+    SR_PTB(20);
+#ifdef SR_PROF
+    {
+        const unsigned long long b0 = __ballot(!(T < e[0]) || (forced & 1u));
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
+            bs.prof[16] += 1;
+            bs.prof[17] += spent == 1u;
+            bs.prof[18] += __popcll(b0);
+        }
+    }
+#endif
     // the others run on: charge them the path since the last event
     float m = INFINITY, mh = INFINITY;
 #pragma unroll
@@ -650,16 +701,18 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
 #ifdef SR_PROF
         if (j < 8 && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[8 + j] += 1;
 #endif
-        const float v = clearance(sc, j, B, a) - perr;
+        sr_dev_slot sl;
+        if (j > 0) sl = pin_slot(sc->slots[j - 1]);
+        const float v = (j == 0 ? clearance_bh(a) : clearance_obj(sl, B, a)) - perr;
         bs.E[j * SR_E_STRIDE] = v;
         m = nmin(m, v);
-        if (j > 0 && ((cyl >> (j - 1)) & 1u)) {
+        if (j > 0 && sl.type == SR_OBJECT_CYLINDER) {
             const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
-            const float vh = clearance_slab(sc->objs[sc->budget_idx[j - 1]], B, a) - perr;
+            const float vh = clearance_slab(sl, B, a) - perr;
             bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
             mh = nmin(mh, vh);
         }
-        if (__ballot(slot_reachable(sc, j, A, B, perr))) reach |= 1u << j;
+        if (__ballot(slot_reachable(&sl, j, A, B, perr))) reach |= 1u << j;
     }
     bs.T = 0.0f;
     bs.m = m;
@@ -1401,7 +1454,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // frag:891-912, the top of step i (the fast loop below leaves a step
         // early whenever some lane's u drops below u_f, so this is where
         // every reseed happens)
-        SR_PT(2);
+        SR_PT(21);
         if (__ballot(r.u < fr.u_f)) {
             if (r.u < fr.u_f) {
                 r.i = i;
@@ -1479,6 +1532,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         else fast(std::false_type{});
         SR_PT(0);
         if (i >= N) break;
+#ifdef SR_PROF
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[19] += 1;
+#endif
         // ---- slow path of step i
         r.i = i;
         r.steps = sbase + i + 1;

@@ -586,6 +586,50 @@ int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers,
     return SR_OK;
 }
 
+// The compact copy of a budgeted object (device_scene.h sr_dev_slot).
+static void pack_slot(const sr_dev_obj& o, int cyl, sr_dev_slot& sl) {
+    std::memset(&sl, 0, sizeof sl);
+    const float* f = o.f;
+    sl.type = o.type;
+    sl.cyl = cyl;
+    sl.rb = o.rb;
+    sl.mp = o.mp;
+    sl.br = o.br;
+    sl.mu = o.mu;
+    sl.pl1 = o.pl1;
+    std::memcpy(sl.bc, o.bc, sizeof sl.bc);
+    std::memcpy(sl.pos, f + SR_F_POS, 3 * sizeof(float));
+    std::memcpy(sl.a0, f + SR_F_AXES, 3 * sizeof(float));
+    std::memcpy(sl.a1, f + SR_F_AXES + 3, 3 * sizeof(float));
+    std::memcpy(sl.a2, f + SR_F_AXES + 6, 3 * sizeof(float));
+    switch (o.type) {
+    case SR_OBJECT_RECTANGLE:
+    case SR_OBJECT_HOLLOW_DISK:
+        sl.x0 = f[17];
+        sl.x1 = f[18];
+        break;
+    case SR_OBJECT_DISK:
+        sl.x0 = f[17];
+        break;
+    case SR_OBJECT_BOX:
+        sl.x0 = f[12];
+        sl.x1 = f[13];
+        sl.x2 = f[14];
+        break;
+    case SR_OBJECT_CYLINDER: {
+        sl.x0 = f[SR_F_P0];
+        sl.x1 = f[SR_F_P0 + 1];
+        // a margin factor: rounded away from zero so the product bounds the
+        // quotient the margin was specified with
+        const double q = (double)SR_CYL_QMARGIN / ((double)sl.x1 * (double)SR_BUDGET_DPMIN);
+        sl.qk = (float)(q * (1.0 + 1e-5));
+        break;
+    }
+    default:
+        break;
+    }
+}
+
 int sr_set_scene(sr_ctx* c, const sr_scene* s) {
     if (!c || !s) return SR_E_INVALID;
     if (s->num_objects < 0 || s->num_lights < 0) return SR_E_INVALID;
@@ -605,6 +649,8 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
         // bounded objects fall back to per-chord bounding-sphere tests
         if (o.kind == SR_KIND_BUDGET && d.num_budget >= SR_MAX_BUDGET) o.kind = SR_KIND_CHORD;
         if (o.kind == SR_KIND_BUDGET) {
+            pack_slot(o, o.type == SR_OBJECT_CYLINDER ? __builtin_popcount((unsigned)d.budget_cyl_mask) : -1,
+                      d.slots[d.num_budget]);
             if (o.type == SR_OBJECT_CYLINDER) d.budget_cyl_mask |= 1 << d.num_budget;
             d.budget_idx[d.num_budget++] = i;
         } else {

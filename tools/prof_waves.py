@@ -15,6 +15,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+NREC = 24  # SR_PROF_N
 SECTIONS = ["fast", "reseed", "slow_entry", "budget_phase1", "exact_chord", "hit_class", "budget_phase2"]
 
 
@@ -47,9 +48,9 @@ def main():
         r.render(cam, params, 1920, 1080, a, b)
     torch.cuda.synchronize()
     nw = ((1920 + 15) // 16) * ((b - a + 15) // 16) * 4
-    buf = (C.c_ulonglong * (16 * nw))()
+    buf = (C.c_ulonglong * (NREC * nw))()
     assert lib.sr_debug_prof(buf, nw) == 0
-    t = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 16).astype(np.int64)
+    t = np.frombuffer(buf, dtype=np.uint64).reshape(nw, NREC).astype(np.int64)
     total = t[:, 7] & ((1 << 48) - 1)
     steps = t[:, 7] >> 48
     ok = total > 0
@@ -63,7 +64,9 @@ def main():
     out["slowest"] = [
         {"wave": int(w), "block_xy": [int(w // 4 % gx), int(w // 4 // gx)], "steps": int(steps[w]),
          "total_cycles": int(total[w]), "cycles_per_step": round(float(total[w]) / max(1, int(steps[w])), 1),
-         **{k: int(v) for k, v in zip(SECTIONS, t[w, :7])}, "reanchors_by_slot": [int(v) for v in t[w, 8:16]]}
+         **{k: int(v) for k, v in zip(SECTIONS, t[w, :7])}, "reanchors_by_slot": [int(v) for v in t[w, 8:16]],
+         "events": int(t[w, 16]), "events_slot0_only": int(t[w, 17]), "lane_slot0_spends": int(t[w, 18]),
+         "slow_entries": int(t[w, 19]), "phase1_ballots": int(t[w, 20]), "tail_top": int(t[w, 21])}
         for w in top]
     print(json.dumps(out, indent=1))
     r.close()
