@@ -442,6 +442,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // event loop indexes it with the wave-uniform slot j in a compact runtime
 // loop, and the step loop's registers hold only T and m.
 #define SR_E_STRIDE 256
+#ifndef SR_AHEAD
+#define SR_AHEAD 2.0f
+#endif
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
 #define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
@@ -629,7 +632,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // slots some lane has spent - usually one - run their clearance and reach
 // tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
-                                                 float perr, uint32_t par, bool reanchor_cyl) {
+                                                 float perr, uint32_t par, bool reanchor_cyl, float ahead) {
     constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -654,7 +657,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     uint32_t spent = 0;  // wave-uniform: slots some lane has spent
 #pragma unroll
     for (int j = 0; j < NS; j++)
-        if (__ballot(!(T < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
+        if (__ballot(!(T + ahead < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
     spent &= (2u << nb) - 1u;
     SR_PTB(20);
 #ifdef SR_PROF
@@ -1543,6 +1546,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return ST_BG;
         }
         const bool event = !(Tn < lim);
+        // slots about to run out re-anchor at this event too (SR_AHEAD steps
+        // of this chord's length ahead): fewer events, each re-anchoring more
+        const float ahead = SR_AHEAD * (Tn - bs.T);
         bs.T = Tn;
         up = r.u;
         r.u = un;
@@ -1571,7 +1577,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
                 // a new frame (reseed): the cylinders' direction tests start over
                 SR_PT(2);
-                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded);
+                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
