@@ -445,6 +445,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
+#ifndef SR_AHEAD_T
+#define SR_AHEAD_T 0.25f
+#endif
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
 #define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
@@ -1546,9 +1549,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return ST_BG;
         }
         const bool event = !(Tn < lim);
-        // slots about to run out re-anchor at this event too (SR_AHEAD steps
-        // of this chord's length ahead): fewer events, each re-anchoring more
-        const float ahead = SR_AHEAD * (Tn - bs.T);
+        // slots about to run out re-anchor at this event too (within SR_AHEAD
+        // of this chord's length plus SR_AHEAD_T of the path since the last
+        // event): fewer events, each re-anchoring more
+        const float ahead = SR_AHEAD * (Tn - bs.T) + SR_AHEAD_T * Tn;
         bs.T = Tn;
         up = r.u;
         r.u = un;
