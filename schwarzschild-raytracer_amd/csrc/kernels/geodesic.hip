@@ -446,7 +446,7 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #define SR_AHEAD 2.0f
 #endif
 #ifndef SR_AHEAD_T
-#define SR_AHEAD_T 0.25f
+#define SR_AHEAD_T 1.0f
 #endif
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
@@ -657,10 +657,13 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             }
         }
     }
-    uint32_t spent = 0;  // wave-uniform: slots some lane has spent
+    uint32_t spent = 0;  // wave-uniform: slots some lane has spent or is about to
+    uint32_t hard = forced;  // this lane's slots whose budget does not cover the chord
 #pragma unroll
-    for (int j = 0; j < NS; j++)
+    for (int j = 0; j < NS; j++) {
+        hard |= (uint32_t)!(T < e[j]) << j;
         if (__ballot(!(T + ahead < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
+    }
     spent &= (2u << nb) - 1u;
     SR_PTB(20);
 #ifdef SR_PROF
@@ -718,7 +721,10 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
             mh = nmin(mh, vh);
         }
-        if (__ballot(slot_reachable(&sl, j, A, B, perr))) reach |= 1u << j;
+        // only lanes whose budget did not cover the chord can reach the slot
+        // (the others re-anchor early: look-ahead, or another lane spent it)
+        const bool h = (hard >> j) & 1u;
+        if (__ballot(h) && __ballot(h && slot_reachable(&sl, j, A, B, perr))) reach |= 1u << j;
     }
     bs.T = 0.0f;
     bs.m = m;
