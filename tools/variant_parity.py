@@ -48,6 +48,22 @@ def main():
         print(f"seed {seed}: {len(bad)} differing pixels")
         for y, x in bad[:10]:
             print(f"   ({x},{y}) gpu steps {s[y, x]} rgba {b[y, x]}  oracle steps {rs[y, x]} rgba {rb[y, x]}")
+    # rays skimming the horizon and orbiting the photon sphere (2000 steps)
+    for name, cam, w, h in [("headline camera", abi.default_camera(), 192, 108),
+                            ("close to the hole", sc.camera_look((0.0, 0.4, 4.0), (0.0, -0.1, -1.0), fov=90.0), 96, 54),
+                            ("edge-on disk", sc.camera_look((9.0, 0.05, 0.0), (-1.0, 0.0, 0.0), fov=40.0), 96, 54)]:
+        scene = sc.scene_default(textured=True)
+        params = abi.default_params(max_steps=2000, percent_black=-1.0)
+        r.set_scene(scene)
+        r.set_test_ray(abi.default_test_ray())
+        f, b, s = r.render_debug(cam, params, w, h)
+        torch.cuda.synchronize()
+        b, s = b.cpu().numpy(), s.cpu().numpy()
+        rb, _, rs = oracle.render(scene, cam, params, w, h, tex)
+        bad = np.argwhere((b != rb).any(-1) | (s != rs))
+        print(f"{name}: {len(bad)} differing pixels")
+        for y, x in bad[:10]:
+            print(f"   ({x},{y}) gpu steps {s[y, x]} rgba {b[y, x]}  oracle steps {rs[y, x]} rgba {rb[y, x]}")
     r.close()
 
 
