@@ -15,6 +15,14 @@
 
 #include <type_traits>
 
+// constant address space: wave-uniform loads through it are scalar loads
+typedef float sr_v4f __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) sr_v4f sr_cfloat4;
+__device__ __forceinline__ float4 ldc(const sr_cfloat4* p) {
+    const sr_v4f v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 #include "../device_scene.h"
 
 namespace {
@@ -1496,7 +1504,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
         // (bs.cm changes only at reseeds, outside the fast loop)
         const bool any_cm = CULL && __ballot(bs.cm != 0u);
-        const float4* __restrict__ tp = tbl + 2 * i;  // {step_size, step_size / 6, cos phi, sin phi}, {g, -, -, -}
+        // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
+        // read through the constant address space: scalar loads
+        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
         float4 e;
         float un, dun, rB, Tn, lim;
         uint32_t par;
@@ -1507,9 +1517,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             constexpr bool CM = decltype(cm_tag)::value;
             lim = lim0;
             par = 0;
+            e = ldc(tp);
+            float4 e1 = ldc(tp + 1);
             for (;;) {
-                e = tp[0];  // wave-uniform scalar loads
-                const float4 e1 = tp[1];  // {g, 0.5 step_size, K_i, -}
+                // the next step's entry, loaded a step ahead (the table holds
+                // max_steps + 1 entries and i + 1 <= N)
+                const float4 en = ldc(tp + 2), e1n = ldc(tp + 3);
+                __builtin_amdgcn_sched_barrier(0);  // issued first: a step of latency to hide
                 rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
                 rB = __builtin_amdgcn_rcpf(un);
                 Tn = bs.T;
@@ -1530,13 +1544,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
                 // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
-                if (__ballot(!(Tn < lim) || un < fr.u_f)) break;
+                if (__ballot(!(Tn < lim) || un < fr.u_f)) {
+                    // a use on the exit path keeps the prefetch where it is
+                    // issued (sunk into the latch it would wait at once)
+                    asm volatile("; keep %0 %1" ::"s"(en.x), "s"(e1n.x));
+                    break;
+                }
                 bs.T = Tn;
                 up = r.u;
                 r.u = un;
                 r.du = dun;
                 rA = rB;
                 tp += 2;
+                e = en;
+                e1 = e1n;
                 if (++i >= N) break;
             }
         };
