@@ -1519,6 +1519,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             par = 0;
             e = ldc(tp);
             float4 e1 = ldc(tp + 1);
+            f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             for (;;) {
                 // the next step's entry, loaded a step ahead (the table holds
                 // max_steps + 1 entries and i + 1 <= N)
@@ -1536,8 +1537,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
                     Tn = __builtin_fmaf(sq, e1.z, Tn);
                     if (CM) {
-                        const f2 p1 = phi_cs(i - 1);
-                        par = chord_parallel(sc, bs, rB * e.z - rA * p1.x, rB * e.w - rA * p1.y, point_err(rA, rB));
+                        par = chord_parallel(sc, bs, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
                         lim = par ? nmin(lim0, bs.mh) : lim0;
                     }
                 }
@@ -1556,6 +1556,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.du = dun;
                 rA = rB;
                 tp += 2;
+                if (CM) pc = F2(e.z, e.w);
                 e = en;
                 e1 = e1n;
                 if (++i >= N) break;
