@@ -67,7 +67,7 @@ def parse():
                     help="noise mask (frag:839-841, 879); the app runs 0.75, the headline -1 (off)")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU, each on its own context and stream (0: min(6, N + 1))")
+                    help="frames in flight per GPU, each on its own context and stream (0: min(6, 2N))")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
@@ -111,9 +111,10 @@ def main():
     # does not shorten; independent frames on their own contexts and streams
     # fill the SIMDs those waves leave idle. Step f renders frame f on context
     # f % F and gathers it to rank 0 on that context's stream.
-    # (measured with tools/inflight.py --shard: one rank's share of an 8-GPU
-    # frame takes 1.98 ms alone, 0.39 ms per frame with 6 in flight)
-    F = args.inflight if args.inflight > 0 else min(6, world + 1)
+    # (measured with tools/inflight.py --shard, profiles/r01/s12_inflight_shards.txt:
+    # one rank's share of an 8-GPU frame takes 1.60 ms alone, 0.34 ms per frame
+    # with 6 in flight; of a 2-GPU frame 0.83 ms with 2, 0.76 ms with 4)
+    F = args.inflight if args.inflight > 0 else min(6, 2 * world)
     skybox = sc.skybox(2048, 1024)
     arr, _, _ = sc.default_texture_array()
     D = pkg.dist

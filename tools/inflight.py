@@ -5,6 +5,7 @@ The frame's time is bounded by its longest rays' waves; with
 several frames in flight the next frames' waves fill the SIMDs those leave idle.
   python tools/inflight.py [--frames 24] [--inflight 1 2 3 4]"""
 import argparse
+import os
 import sys
 import time
 from pathlib import Path
@@ -22,9 +23,10 @@ def main():
                     help="render only this rank's block-cyclic share of an N-GPU frame (8-row blocks)")
     args = ap.parse_args()
     if args.lib:
-        import os
-
         os.environ["SR_LIB"] = str(Path(args.lib).resolve())
+    # as bench.py: every in-flight frame's stream gets a hardware queue
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     import torch
 
     import srpkg
