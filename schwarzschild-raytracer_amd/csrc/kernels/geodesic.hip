@@ -339,12 +339,18 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // direction are tested per chord instead (budget_parallel). Computed with
 // hardware sqrt: its error is far below the margins.
 #define SR_PATH_SLACK 1.01f
+#ifndef SR_NEAR
+#define SR_NEAR 1.0f
+#endif
 __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, float a) {
     float c;
     {
         f3 w = A - ld3(sl.bc);
         c = __builtin_amdgcn_sqrtf(dot(w, w)) - sl.rb;
-        if (sl.mp < INFINITY) {  // distance to the primitive itself (orthonormal frame)
+        // distance to the primitive itself (orthonormal frame). When every lane
+        // of the wave is far from the object (beyond SR_NEAR (rb + 1) of its
+        // bounding sphere) that sphere's distance is close to it: skip it.
+        if (sl.mp < INFINITY && __ballot(c < SR_NEAR * (sl.rb + 1.0f))) {
             const f3 q = A - ld3(sl.pos);
             const float y = dot(q, ld3(sl.a1));  // along axes[1] (plane normal / height)
             float d2;
