@@ -318,3 +318,22 @@ def test_test_ray_far_view(pkg, gpu, oracle, oracle_tex):
     compare(g, o, "test ray far view")
     assert (g[0][..., :3] != o[0][..., :3]).sum() == 0
     gpu.set_test_ray(abi.default_test_ray())
+
+
+@pytest.mark.parametrize("name,pos,fwd,fov,textured", [
+    ("close to the hole", (0.0, 0.4, 4.0), (0.0, -0.1, -1.0), 90.0, True),
+    ("edge-on accretion disk", (9.0, 0.05, 0.0), (-1.0, 0.0, 0.0), 40.0, True),
+    ("photon ring, untextured", (0.0, 3.0, 14.0), (0.0, -3.0, -14.0), 25.0, False),
+])
+def test_near_horizon_views(pkg, gpu, oracle, oracle_tex, name, pos, fwd, fov, textured):
+    """Rays skimming the r = 1 shell and orbiting the photon sphere for up to
+    2000 steps: the black hole's shell clearance, the budget look-ahead and
+    the re-anchor shortcuts where budget events are densest."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=textured)
+    cam = sc.camera_look(pos, fwd, fov=fov)
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, cam, params, 96, 54)
+    o = oracle.render(scene, cam, params, 96, 54, oracle_tex)
+    compare(g, o, name)
+    assert (g[2] != o[2]).sum() == 0, f"{name}: step counts differ"
