@@ -724,21 +724,43 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
 #ifdef SR_PROF
         if (j < 8 && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[8 + j] += 1;
 #endif
-        sr_dev_slot sl;
-        if (j > 0) sl = pin_slot(sc->slots[j - 1]);
-        const float v = (j == 0 ? clearance_bh(a) : clearance_obj(sl, B, a)) - perr;
-        bs.E[j * SR_E_STRIDE] = v;
-        m = nmin(m, v);
-        if (j > 0 && sl.type == SR_OBJECT_CYLINDER) {
-            const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
-            const float vh = clearance_slab(sl, B, a) - perr;
-            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
-            mh = nmin(mh, vh);
-        }
         // only lanes whose budget did not cover the chord can reach the slot
         // (the others re-anchor early: look-ahead, or another lane spent it)
         const bool h = (hard >> j) & 1u;
-        if (__ballot(h) && __ballot(h && slot_reachable(&sl, j, A, B, perr))) reach |= 1u << j;
+        if (j == 0) {
+            const float v = clearance_bh(a) - perr;
+            bs.E[0] = v;
+            m = nmin(m, v);
+            if (__ballot(h) && __ballot(h && slot_reachable(nullptr, 0, A, B, perr))) reach |= 1u;
+            continue;
+        }
+        const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);
+        // One straight-line copy per object type (the type a compile-time
+        // constant in it): the clearance and the reach test interleave.
+        auto reanchor = [&](auto ty_tag) {
+            constexpr int TY = decltype(ty_tag)::value;
+            sr_dev_slot st = sl;
+            st.type = TY;
+            const float v = clearance_obj(st, B, a) - perr;
+            bs.E[j * SR_E_STRIDE] = v;
+            m = nmin(m, v);
+            if (TY == SR_OBJECT_CYLINDER) {
+                const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
+                const float vh = clearance_slab(st, B, a) - perr;
+                bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
+                mh = nmin(mh, vh);
+            }
+            if (__ballot(h) && __ballot(h && slot_reachable(&st, j, A, B, perr))) reach |= 1u << j;
+        };
+        switch (sl.type) {
+        case SR_OBJECT_DISK: reanchor(std::integral_constant<int, SR_OBJECT_DISK>{}); break;
+        case SR_OBJECT_HOLLOW_DISK: reanchor(std::integral_constant<int, SR_OBJECT_HOLLOW_DISK>{}); break;
+        case SR_OBJECT_RECTANGLE: reanchor(std::integral_constant<int, SR_OBJECT_RECTANGLE>{}); break;
+        case SR_OBJECT_BOX: reanchor(std::integral_constant<int, SR_OBJECT_BOX>{}); break;
+        case SR_OBJECT_CYLINDER: reanchor(std::integral_constant<int, SR_OBJECT_CYLINDER>{}); break;
+        case SR_OBJECT_PLANE: reanchor(std::integral_constant<int, SR_OBJECT_PLANE>{}); break;
+        default: reanchor(std::integral_constant<int, SR_OBJECT_SPHERE>{}); break;
+        }
     }
     bs.T = 0.0f;
     bs.m = m;
