@@ -334,9 +334,10 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // with rb = bounding radius + mu_q (1 + |c|_1 + R) and the path slack covering
 // the T-proportional part of the rounding margins. Cylinders also subtract
 // their quadratic margin SR_CYL_QMARGIN S^2 / (r SR_BUDGET_DPMIN) for the
-// largest S a chord of the window can have (windows are capped at
-// SR_BUDGET_TMAX); chords closer than SR_BUDGET_DPMIN to the cylinder axis
-// direction are tested per chord instead (budget_parallel). Computed with
+// largest S a chord of the window can have (a window is at most the
+// clearance before this margin, capped at SR_BUDGET_TMAX); chords closer than
+// SR_BUDGET_DPMIN to the cylinder axis direction are covered by the slab
+// budget instead (clearance_slab, chord_parallel). Computed with
 // hardware sqrt: its error is far below the margins.
 #define SR_PATH_SLACK 1.01f
 #ifndef SR_NEAR
@@ -380,7 +381,10 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
         if (sl.type == SR_OBJECT_CYLINDER) {
             // quadratic margin SR_CYL_QMARGIN Sb^2 / (r SR_BUDGET_DPMIN), the
             // quotient folded into sl.qk on the host
-            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + (3.0f * SR_BUDGET_TMAX + 1.0f);
+            // the window's path is at most this clearance (capped): chord
+            // origins stay within sqrt(3) W of A, chords within W long
+            const float W = fminf(c, SR_BUDGET_TMAX);
+            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + (3.0f * W + 1.0f);
             float qm = (Sb * Sb) * sl.qk;
             c = fminf(c - qm, SR_BUDGET_TMAX);
         }
