@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU, each on its own context and stream (0: min(6, 2N))")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--critical-path", choices=["on", "off"], default="on",
+                    help="time the slowest row bands alone (extra launches of the same kernel; off for rocprof stats)")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
@@ -204,7 +206,7 @@ def main():
     # so the frame's launch-order state stays untouched. Its time is the
     # slowest waves' latency without contention.
     critical = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and args.critical_path == "on":
         rb = pkg.Renderer(local)
         rb.set_scene(scene)
         rb.set_background(skybox)

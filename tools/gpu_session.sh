@@ -28,7 +28,7 @@ if [[ $STEPS == *bench* ]]; then
   grep '^{' "$OUT/bench.log" > "$OUT/bench.json"
 fi
 if [[ $STEPS == *prof* ]]; then
-  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-baseline off || exit $?
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-baseline off --critical-path off || exit $?
   find "$OUT/prof" -name "*stats*" -o -name "*kernel_stats*" | head -20
 fi
 echo "session done"
