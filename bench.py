@@ -115,8 +115,12 @@ def main():
     # f % F and gathers it to rank 0 on that context's stream.
     # (measured with tools/inflight.py --shard, profiles/r01/s12_inflight_shards.txt:
     # one rank's share of an 8-GPU frame takes 1.60 ms alone, 0.34 ms per frame
-    # with 6 in flight; of a 2-GPU frame 0.83 ms with 2, 0.76 ms with 4)
-    F = args.inflight if args.inflight > 0 else min(6, 2 * world)
+    # with 6 in flight; of a 2-GPU frame 0.83 ms with 2, 0.76 ms with 4).
+    # What matters is the rank's pixel count, so a smaller frame (config 2)
+    # gets more in flight the same way: 2 per 1080p-frame's worth of rows
+    # over the rank's share, between 2 and 6 (headline: min(6, 2N)).
+    share = W * H / world
+    F = args.inflight if args.inflight > 0 else max(2, min(6, round(2 * 1920 * 1080 / share)))
     skybox = sc.skybox(2048, 1024)
     arr, _, _ = sc.default_texture_array()
     D = pkg.dist
