@@ -67,7 +67,7 @@ def parse():
                     help="noise mask (frag:839-841, 879); the app runs 0.75, the headline -1 (off)")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU, each on its own context and stream (0: min(6, 2N))")
+                    help="frames in flight per GPU, each on its own context and stream (0: 4, or 6 when the rank holds under a quarter of a 1080p frame)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--critical-path", choices=["on", "off"], default="on",
                     help="time the slowest row bands alone (extra launches of the same kernel; off for rocprof stats)")
@@ -116,11 +116,12 @@ def main():
     # (measured with tools/inflight.py --shard, profiles/r01/s12_inflight_shards.txt:
     # one rank's share of an 8-GPU frame takes 1.60 ms alone, 0.34 ms per frame
     # with 6 in flight; of a 2-GPU frame 0.83 ms with 2, 0.76 ms with 4).
-    # What matters is the rank's pixel count, so a smaller frame (config 2)
-    # gets more in flight the same way: 2 per 1080p-frame's worth of rows
-    # over the rank's share, between 2 and 6 (headline: min(6, 2N)).
+    # What matters is the rank's pixel count: 4 in flight while a rank holds at
+    # least a quarter of a 1080p frame, 6 below that (an 8-GPU share, config 2).
+    # Re-measured at N = 1 (profiles/r01/s18_inflight_headline.jsonl): 2 / 3 /
+    # 4 / 6 in flight give 1.44 / 1.41 / 1.41 / 1.41 ms per frame.
     share = W * H / world
-    F = args.inflight if args.inflight > 0 else max(2, min(6, round(2 * 1920 * 1080 / share)))
+    F = args.inflight if args.inflight > 0 else (4 if share >= 1920 * 1080 / 4 else 6)
     skybox = sc.skybox(2048, 1024)
     arr, _, _ = sc.default_texture_array()
     D = pkg.dist
