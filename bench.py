@@ -50,6 +50,12 @@ WORKLOADS = {
 MODES = {"curved": 0, "flat": 1, "half_width": 2, "half_height": 3}
 
 
+def frames_in_flight(width, height, world):
+    """Default frames in flight per GPU: 4 while a rank holds at least a
+    quarter of a 1080p frame, 6 below that."""
+    return 4 if width * height / world >= 1920 * 1080 / 4 else 6
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,8 +126,7 @@ def main():
     # least a quarter of a 1080p frame, 6 below that (an 8-GPU share, config 2).
     # Re-measured at N = 1 (profiles/r01/s18_inflight_headline.jsonl): 2 / 3 /
     # 4 / 6 in flight give 1.44 / 1.41 / 1.41 / 1.41 ms per frame.
-    share = W * H / world
-    F = args.inflight if args.inflight > 0 else (4 if share >= 1920 * 1080 / 4 else 6)
+    F = args.inflight if args.inflight > 0 else frames_in_flight(W, H, world)
     skybox = sc.skybox(2048, 1024)
     arr, _, _ = sc.default_texture_array()
     D = pkg.dist

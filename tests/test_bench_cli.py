@@ -52,3 +52,12 @@ def test_workloads_match_baseline_configs():
 def test_help_runs_without_a_gpu():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "--workload" in r.stdout and "--inflight" in r.stdout
+
+
+def test_frames_in_flight_by_rank_share():
+    import bench
+
+    # headline: 4 up to N = 4 (s12/s18 optimum per share), 6 at N = 8
+    assert [bench.frames_in_flight(1920, 1080, n) for n in (1, 2, 4, 8)] == [4, 4, 4, 6]
+    assert bench.frames_in_flight(640, 360, 1) == 6  # config 2
+    assert bench.frames_in_flight(3840, 2160, 1) == 4
