@@ -83,6 +83,36 @@ def default_texture_array():
     return pad_texture_array([uv_checker(600), cubemap(1601, 1201)])
 
 
+def feature_texture_array():
+    """Texture array of the material-flag scene (scene_features): layer 0 a
+    smaller translucent RGBA gradient (alpha 96..208, never 255; zero-padded;
+    gradients of at most ~1.3 levels per texel, so a ray that lands a small
+    fraction of a texel away on another GL implementation reads nearly the
+    same colour, while swapped or inverted uv still change it),
+    layer 1 a full-size RGB normal map (alpha 255). Every textured hit is
+    translucent, so rays go on past it under every GL filter implementation:
+    SwiftShader's 16-bit filter, whose alpha is never exactly 1 (DESIGN.md
+    §3), then pins the textured paths too. The normal map has no padding and
+    no zero texel: planes sample it at uv beyond [0, 1] (GL_REPEAT over the
+    whole layer), and normalize(0) is undefined in GLSL (frag:409)."""
+    w, h = 200, 150
+    x = np.arange(w, dtype=np.int64)[None, :]
+    y = np.arange(h, dtype=np.int64)[:, None]
+    r = 40 + (x * y * 180) // ((w - 1) * (h - 1))
+    g = (x * 255) // (w - 1) + 0 * y
+    b = (y * 255) // (h - 1) + 0 * x
+    a = 96 + (x * 112) // (w - 1) + 0 * y
+    layer0 = np.stack([r, g, b, a], axis=-1).astype(np.uint8)
+    nw, nh = 256, 192
+    x = np.arange(nw, dtype=np.int64)[None, :]
+    y = np.arange(nh, dtype=np.int64)[:, None]
+    nr = 64 + (x * 128) // (nw - 1) + 0 * y
+    ng = 64 + (y * 128) // (nh - 1) + 0 * x
+    nb = 200 + 0 * x + 0 * y
+    layer1 = np.stack([nr, ng, nb], axis=-1).astype(np.uint8)
+    return pad_texture_array([layer0, layer1])
+
+
 # ---- scenes --------------------------------------------------------------------
 def scene_default(textured: bool = True) -> abi.Scene:
     """src/main.cpp:222-268 packed by the library's ObjectLoader mirror."""
@@ -201,6 +231,107 @@ def scene_random(seed: int, n_objects: int = 21, translucent: bool = True, plane
         o.type, o.index, o.material_index = t, k, int(rng.integers(0, abi.MAX_MATERIALS))
         n += 1
     s.num_objects = n
+    return s
+
+
+def _axes_from(up, ref=(1.0, 0.0, 0.0)) -> list[float]:
+    """Column-major orthonormal axes with axes[1] = normalize(up) (the plane
+    normal / cylinder axis) and axes[0] in the plane of ref, float32."""
+    u = np.asarray(up, dtype=np.float64)
+    u = u / np.linalg.norm(u)
+    a = np.asarray(ref, dtype=np.float64)
+    a = a - u * np.dot(a, u)
+    a = a / np.linalg.norm(a)
+    c = np.cross(a, u)
+    return [float(np.float32(v)) for v in (*a, *u, *c)]
+
+
+def scene_features() -> abi.Scene:
+    """The material-flag scene pinned by SwiftShader goldens (golden_r2):
+    two planes (texture offset, size, repeat on/off), every primitive type
+    once, 8 materials covering the calculate_lighting paths (frag:365-438):
+    translucent textures, normal maps, swap / invert uv (plane-size aware
+    inversion), single-sided and flipped normals, alpha < 1 - and 4 lights
+    (the reference's MAX_LIGHTS). Textures: feature_texture_array()."""
+    s = abi.Scene()
+    abi.load().sr_scene_clear(C.byref(s))
+    set_scene_texture_sizes(s, [(200, 150), (256, 192)], (256, 192))
+
+    def mat(m, color, tex=-1, nmap=-1, inv_x=0, inv_y=0, swap=0, double=1, flip=0, amb=0.1, dif=0.9, spec=0.5,
+            shin=32.0):
+        M = s.materials[m]
+        for k in range(4):
+            M.color[k] = float(np.float32(color[k]))
+        M.ambient, M.diffuse, M.specular, M.shininess = amb, dif, spec, shin
+        M.texture_index, M.normal_map_index = tex, nmap
+        M.invert_uv_x, M.invert_uv_y, M.swap_uvs = inv_x, inv_y, swap
+        M.double_sided_normals, M.flip_normals = double, flip
+
+    mat(0, (0.5, 0.0, 0.5, 1.0), tex=0, inv_x=1)                      # plane 0: textured, plane-size invert x
+    mat(1, (0.5, 0.0, 0.5, 1.0), tex=0, nmap=1, swap=1)               # sphere: normal map + swap
+    mat(2, (0.2, 0.8, 0.3, 1.0), double=0)                            # disk: single-sided, opaque
+    mat(3, (0.9, 0.6, 0.1, 0.5), double=0, flip=1)                    # hollow disk: flipped, single-sided, alpha .5
+    mat(4, (0.5, 0.0, 0.5, 1.0), tex=0, nmap=1, inv_y=1, spec=0.9, shin=8.0)  # cylinder
+    mat(5, (0.3, 0.4, 0.9, 0.5), spec=1.0, shin=4.0)                  # rectangle: alpha .5
+    mat(6, (0.5, 0.0, 0.5, 1.0), tex=0, swap=1, inv_x=1, inv_y=1, flip=1)  # box: every uv flag, flipped
+    mat(7, (0.5, 0.0, 0.5, 1.0), tex=0, nmap=1, swap=1, inv_y=1, double=0)  # plane 1: single-sided
+
+    def tr(t, pos, axes):
+        for i in range(3):
+            t.pos[i] = float(np.float32(pos[i]))
+        for i in range(9):
+            t.axes[i] = axes[i]
+
+    ident = [1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0]
+    objs = []
+    p0 = s.planes[0]
+    tr(p0.transform, (0.0, -4.0, 0.0), ident)
+    p0.texture_offset[0], p0.texture_offset[1] = -2.0, -1.5
+    p0.repeat_texture = 0  # far, grazing hits of an infinite plane are ill-conditioned: texture a patch
+    p0.texture_size[0], p0.texture_size[1] = 5.0, 4.0
+    objs.append((abi.OBJECT_PLANE, 0, 0))
+    p1 = s.planes[1]
+    tr(p1.transform, (0.0, 0.0, -30.0), _axes_from((0.0, 0.0, 1.0)))
+    p1.texture_offset[0], p1.texture_offset[1] = -0.5, 0.1
+    p1.repeat_texture = 1
+    p1.texture_size[0], p1.texture_size[1] = 4.0, 3.0
+    objs.append((abi.OBJECT_PLANE, 1, 7))
+    tr(s.spheres[0].transform, (-6.0, 1.0, 0.0), _axes_from((0.3, 1.0, 0.2)))
+    s.spheres[0].radius = 1.5
+    objs.append((abi.OBJECT_SPHERE, 0, 1))
+    tr(s.disks[0].plane.transform, (0.0, 0.0, -8.0), _axes_from((0.4, 0.3, 1.0)))
+    s.disks[0].radius = 2.0
+    objs.append((abi.OBJECT_DISK, 0, 2))
+    tr(s.hollow_disks[0].plane.transform, (0.0, 0.0, 0.0), _axes_from((0.05, 1.0, 0.1)))
+    s.hollow_disks[0].inner_radius, s.hollow_disks[0].outer_radius = 2.5, 5.0
+    objs.append((abi.OBJECT_HOLLOW_DISK, 0, 3))
+    tr(s.cylinders[0].transform, (0.0, 6.0, 0.0), _axes_from((0.2, 1.0, -0.1)))
+    s.cylinders[0].height, s.cylinders[0].radius = 4.0, 1.5
+    objs.append((abi.OBJECT_CYLINDER, 0, 4))
+    tr(s.rectangles[0].plane.transform, (3.0, -1.0, 8.0), _axes_from((0.0, 0.3, 1.0)))
+    s.rectangles[0].width, s.rectangles[0].height = 3.0, 2.0
+    objs.append((abi.OBJECT_RECTANGLE, 0, 5))
+    tr(s.boxes[0].transform, (7.0, 0.0, -2.0), _axes_from((0.2, 1.0, 0.3), (1.0, 0.0, 1.0)))
+    s.boxes[0].width, s.boxes[0].depth, s.boxes[0].height = 1.5, 1.0, 2.0
+    objs.append((abi.OBJECT_BOX, 0, 6))
+    for n, (t, k, m) in enumerate(objs):
+        o = s.objects[n]
+        o.type, o.index, o.material_index = t, k, m
+    s.num_objects = len(objs)
+    lights = [((10.0, 10.0, 10.0), (1.0, 1.0, 1.0), 8.0, (1.0, 0.09, 0.032)),
+              ((-12.0, 4.0, 6.0), (1.0, 0.6, 0.3), 6.0, (1.0, 0.05, 0.01)),
+              ((0.0, -10.0, 12.0), (0.3, 0.5, 1.0), 10.0, (0.5, 0.1, 0.02)),
+              ((4.0, 15.0, -10.0), (0.8, 1.0, 0.8), 5.0, (1.0, 0.0, 0.05))]
+    s.num_lights = len(lights)
+    for i, (pos, col, inten, att) in enumerate(lights):
+        L = s.lights[i]
+        for k in range(3):
+            L.transform.pos[k] = pos[k]
+            L.color[k] = col[k]
+        for k in range(9):
+            L.transform.axes[k] = ident[k]
+        L.intensity = inten
+        L.attenuation_constant, L.attenuation_linear, L.attenuation_quadratic = att
     return s
 
 

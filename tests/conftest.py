@@ -11,6 +11,30 @@ if str(ROOT) not in sys.path:
 import srpkg  # noqa: E402
 
 GOLDEN = ROOT / "tests" / "golden" / "golden.npz"
+GOLDEN_R2 = ROOT / "tests" / "golden" / "golden_r2.npz"  # reseed, config 2, material flags
+
+
+class Golden:
+    """The golden fixture files as one mapping (case keys are unique across
+    files; meta_cases is the concatenation of their case lists)."""
+
+    def __init__(self, paths):
+        self.parts = [np.load(p) for p in paths]
+
+    def __contains__(self, key):
+        return any(key in p for p in self.parts)
+
+    def __getitem__(self, key):
+        for p in self.parts:
+            if key in p:
+                return p[key]
+        raise KeyError(key)
+
+    def cases(self):
+        out = []
+        for p in self.parts:
+            out += bytes(p["meta_cases"]).decode().split("\n")
+        return out
 
 
 def pytest_configure(config):
@@ -30,14 +54,14 @@ def oracle():
 
 @pytest.fixture(scope="session")
 def golden():
-    if not GOLDEN.exists():
-        pytest.skip("golden.npz missing (python tests/golden/make_golden.py)")
-    return np.load(GOLDEN)
+    if not GOLDEN.exists() or not GOLDEN_R2.exists():
+        pytest.skip("golden fixtures missing (python tests/golden/make_golden.py [--set r2])")
+    return Golden([GOLDEN, GOLDEN_R2])
 
 
 @pytest.fixture(scope="session")
 def golden_cases(golden):
-    return bytes(golden["meta_cases"]).decode().split("\n")
+    return golden.cases()
 
 
 @pytest.fixture(scope="session")
@@ -47,6 +71,17 @@ def textures(pkg, golden):
     bg = sc.skybox(w, h)
     arr, _, _ = sc.default_texture_array()
     return bg, arr
+
+
+def case_texture_kind(golden, name) -> str:
+    """'default' (scenes.default_texture_array) or 'features'
+    (scenes.feature_texture_array)."""
+    return bytes(golden[name + "/textures"]).decode() if name + "/textures" in golden else "default"
+
+
+def texture_array_of(pkg, kind):
+    sc = pkg.scenes
+    return (sc.feature_texture_array() if kind == "features" else sc.default_texture_array())[0]
 
 
 def load_case(pkg, golden, name):

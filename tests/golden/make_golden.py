@@ -20,6 +20,7 @@ Inputs are the library's own scene/camera structs (sr_default_scene =
 the C++ mirror of src/main.cpp:222-268) and integer-procedural textures, so the
 goldens do not depend on a JPEG decoder. Run in the build container:
     python tests/golden/make_golden.py            # writes tests/golden/golden.npz
+    python tests/golden/make_golden.py --set r2   # writes tests/golden/golden_r2.npz
 """
 from __future__ import annotations
 
@@ -61,9 +62,17 @@ ES_CAPACITIES = {
     "MAX_DISKS": 1, "MAX_HOLLOW_DISKS": 1, "MAX_CYLINDERS": 1, "MAX_RECTANGLES": 1, "MAX_BOXES": 1,
     "MAX_POINTS": 8,
 }
+# Capacity profiles: the 261 uniform vectors are traded between features.
+# "features" gives up the press-R polyline (MAX_POINTS 1) for the reference's
+# full 4 lights, 8 materials and 2 planes (the material-flag scene, cases_r2;
+# 10 materials do not fit).
+ES_PROFILES = {
+    "default": ES_CAPACITIES,
+    "features": dict(ES_CAPACITIES, MAX_LIGHTS=4, MAX_MATERIALS=8, MAX_PLANES=2, MAX_POINTS=1),
+}
 
 
-def es_sources(steps_variant: bool = False) -> tuple[str, str]:
+def es_sources(steps_variant: bool = False, caps: dict | None = None) -> tuple[str, str]:
     vert = (REF_SHADERS / "full_screen_quad.vert").read_text()
     frag = (REF_SHADERS / "black_hole.frag").read_text()
     vert = vert.replace("#version 330 core", "#version 300 es")
@@ -87,7 +96,7 @@ def es_sources(steps_variant: bool = False) -> tuple[str, str]:
             raise RuntimeError(f"ES edit anchor not found: {a!r}")
         frag = frag.replace(a, b)
     # 5. capacities
-    for k, v in ES_CAPACITIES.items():
+    for k, v in (caps or ES_CAPACITIES).items():
         frag, n = re.subn(rf"#define {k} \d+", f"#define {k} {v}", frag)
         if n != 1:
             raise RuntimeError(f"capacity {k} not found")
@@ -171,11 +180,12 @@ class SwiftShader:
             raise RuntimeError("shader compile failed:\n" + log.value.decode())
         return sh
 
-    def program(self, steps_variant=False):
-        if steps_variant in self.programs:
-            return self.programs[steps_variant]
+    def program(self, steps_variant=False, profile="default"):
+        key = (steps_variant, profile)
+        if key in self.programs:
+            return self.programs[key]
         gl = self.gl
-        vs, fs = es_sources(steps_variant)
+        vs, fs = es_sources(steps_variant, ES_PROFILES[profile])
         prog = gl.glCreateProgram()
         gl.glAttachShader(prog, self._compile(GL_VERTEX_SHADER, vs))
         gl.glAttachShader(prog, self._compile(GL_FRAGMENT_SHADER, fs))
@@ -186,7 +196,7 @@ class SwiftShader:
             log = C.create_string_buffer(8192)
             gl.glGetProgramInfoLog(prog, 8192, None, log)
             raise RuntimeError("link failed:\n" + log.value.decode())
-        self.programs[steps_variant] = prog
+        self.programs[key] = prog
         return prog
 
     # ---- uniforms ----------------------------------------------------------------
@@ -219,10 +229,12 @@ class SwiftShader:
         self.u1i(prog, prefix + ".repeat_texture", p.repeat_texture)
         self.u2f(prog, prefix + ".texture_size", p.texture_size)
 
-    def set_uniforms(self, prog, scene, cam, params, test_ray, width, height):
+    def set_uniforms(self, prog, scene, cam, params, test_ray, width, height, caps=None):
         """What Camera::loadShader, ObjectLoader::load, loadTextureArray and the
         main loop upload (src/main.cpp:272-297, 377-429)."""
         gl = self.gl
+        caps = caps or ES_CAPACITIES
+        assert scene.num_lights <= caps["MAX_LIGHTS"], "scene exceeds the ES light capacity"
         gl.glUseProgram(prog)
         self.u1i(prog, "background_texture", 0)
         self.u1i(prog, "textures", 1)
@@ -246,10 +258,10 @@ class SwiftShader:
             self.u1f(prog, pre + ".attenuation_constant", L.attenuation_constant)
             self.u1f(prog, pre + ".attenuation_linear", L.attenuation_linear)
             self.u1f(prog, pre + ".attenuation_quadratic", L.attenuation_quadratic)
-        for i in range(ES_CAPACITIES["MAX_TEXTURES"]):
+        for i in range(caps["MAX_TEXTURES"]):
             self.u2f(prog, f"texture_sizes[{i}]", scene.texture_sizes[i])
         self.u2f(prog, "max_texture_size", scene.max_texture_size)
-        for m in range(ES_CAPACITIES["MAX_MATERIALS"]):
+        for m in range(caps["MAX_MATERIALS"]):
             M, pre = scene.materials[m], f"materials[{m}]"
             self.u4f(prog, pre + ".color", M.color)
             for f in ("ambient", "diffuse", "specular", "shininess"):
@@ -263,27 +275,27 @@ class SwiftShader:
             self.u1i(prog, f"objects[{i}].type", o.type)
             self.u1i(prog, f"objects[{i}].index", o.index)
             self.u1i(prog, f"objects[{i}].material_index", o.material_index)
-        for k in range(ES_CAPACITIES["MAX_SPHERES"]):
+        for k in range(caps["MAX_SPHERES"]):
             self.utransform(prog, f"spheres[{k}].transform", scene.spheres[k].transform)
             self.u1f(prog, f"spheres[{k}].radius", scene.spheres[k].radius)
-        for k in range(ES_CAPACITIES["MAX_PLANES"]):
+        for k in range(caps["MAX_PLANES"]):
             self.uplane(prog, f"planes[{k}]", scene.planes[k])
-        for k in range(ES_CAPACITIES["MAX_DISKS"]):
+        for k in range(caps["MAX_DISKS"]):
             self.uplane(prog, f"disks[{k}].plane", scene.disks[k].plane)
             self.u1f(prog, f"disks[{k}].radius", scene.disks[k].radius)
-        for k in range(ES_CAPACITIES["MAX_HOLLOW_DISKS"]):
+        for k in range(caps["MAX_HOLLOW_DISKS"]):
             self.uplane(prog, f"hollow_disks[{k}].plane", scene.hollow_disks[k].plane)
             self.u1f(prog, f"hollow_disks[{k}].inner_radius", scene.hollow_disks[k].inner_radius)
             self.u1f(prog, f"hollow_disks[{k}].outer_radius", scene.hollow_disks[k].outer_radius)
-        for k in range(ES_CAPACITIES["MAX_CYLINDERS"]):
+        for k in range(caps["MAX_CYLINDERS"]):
             self.utransform(prog, f"cylinders[{k}].transform", scene.cylinders[k].transform)
             self.u1f(prog, f"cylinders[{k}].height", scene.cylinders[k].height)
             self.u1f(prog, f"cylinders[{k}].radius", scene.cylinders[k].radius)
-        for k in range(ES_CAPACITIES["MAX_RECTANGLES"]):
+        for k in range(caps["MAX_RECTANGLES"]):
             self.uplane(prog, f"rectangles[{k}].plane", scene.rectangles[k].plane)
             self.u1f(prog, f"rectangles[{k}].width", scene.rectangles[k].width)
             self.u1f(prog, f"rectangles[{k}].height", scene.rectangles[k].height)
-        for k in range(ES_CAPACITIES["MAX_BOXES"]):
+        for k in range(caps["MAX_BOXES"]):
             b = scene.boxes[k]
             self.utransform(prog, f"boxes[{k}].transform", b.transform)
             self.u1f(prog, f"boxes[{k}].width", b.width)
@@ -298,7 +310,7 @@ class SwiftShader:
         self.u3f(prog, "test_ray_flat_origin", tr.flat_origin)
         self.u3f(prog, "test_ray_flat_dir", tr.flat_dir)
         self.u1i(prog, "num_test_ray_curved_points", tr.num_curved_points)
-        for i in range(min(tr.num_curved_points, ES_CAPACITIES["MAX_POINTS"])):
+        for i in range(min(tr.num_curved_points, caps["MAX_POINTS"])):
             self.u3f(prog, f"test_ray_curved_points[{i}]", tr.curved_points[i])
 
     # ---- textures ----------------------------------------------------------------
@@ -356,10 +368,11 @@ class SwiftShader:
         gl.glDeleteRenderbuffers(1, C.byref(rb))
         return out  # rows bottom-up (GL order), like the kernel's output
 
-    def render(self, scene, cam, params, width, height, test_ray=None, steps_variant=False, float_target=False):
-        prog = self.program(steps_variant)
+    def render(self, scene, cam, params, width, height, test_ray=None, steps_variant=False, float_target=False,
+               profile="default"):
+        prog = self.program(steps_variant, profile)
         tr = test_ray if test_ray is not None else abi.default_test_ray()
-        self.set_uniforms(prog, scene, cam, params, tr, width, height)
+        self.set_uniforms(prog, scene, cam, params, tr, width, height, ES_PROFILES[profile])
         return self.draw(prog, width, height, float_target)
 
 
@@ -413,7 +426,46 @@ def cases():
     return out
 
 
+def cases_r2():
+    """Round-2 goldens (golden_r2.npz): the u < u_f reseed branch (frag:891-912,
+    phi not reset) from cameras beyond r = 1/u_f and with u_f = 0.1, the
+    640x360 / 1000-step frame of BASELINE config 2, and the material-flag
+    scene (scenes.scene_features: planes, normal maps, uv flags, single-sided,
+    flipped and translucent materials, 4 lights) under the "features" ES
+    capacity profile."""
+    P = abi.default_params
+    dcam = abi.default_camera()
+    far120 = sc.camera_look((0.0, 12.0, 119.4), (0.0, -12.0, -119.4), fov=12.0)
+    far300 = sc.camera_look((60.0, 40.0, 291.2), (-60.0, -40.0, -291.2), fov=5.0)
+    side = sc.camera_look((-150.0, 3.0, 40.0), (150.0, -3.0, -41.0), fov=8.0)
+    feat = {"profile": "features", "textures": "features"}
+    out = [
+        ("reseed_r120", "untex", far120, P(max_steps=1000, percent_black=-1.0), 160, 90, None,
+         {"steps": True, "float": True}),
+        ("reseed_r300", "untex", far300, P(max_steps=1000, percent_black=-1.0), 160, 90, None, {"steps": True}),
+        ("reseed_side", "bh", side, P(max_steps=1000, percent_black=-1.0), 128, 72, None, {"steps": True}),
+        ("reseed_uf01", "untex", dcam, P(max_steps=1000, percent_black=-1.0, u_f=0.1), 160, 90, None,
+         {"steps": True, "float": True}),
+        ("reseed_uf005_far", "untex", far120, P(max_steps=600, percent_black=-1.0, u_f=0.05), 96, 54, None,
+         {"steps": True}),
+        ("config2_640x360", "untex", dcam, P(max_steps=1000, percent_black=-1.0), 640, 360, None, {"steps": True}),
+    ]
+    fcams = [
+        ("features_default", dcam, 0),
+        ("features_oblique", sc.camera_look((12.0, 8.0, 14.0), (-12.0, -8.0, -14.0), fov=70.0), 0),
+        ("features_low", sc.camera_look((-3.0, -2.5, 12.0), (3.0, 1.5, -12.0), fov=80.0), 0),
+        ("features_below", sc.camera_look((2.0, -7.0, 10.0), (-2.0, 6.0, -10.0), fov=75.0), 0),
+        ("features_flat", sc.camera_look((12.0, 8.0, 14.0), (-12.0, -8.0, -14.0), fov=70.0), 1),
+    ]
+    for name, cam, mode in fcams:
+        ex = dict(feat, steps=mode == 0, float=name == "features_default")
+        out.append((name, "features", cam, P(max_steps=600, percent_black=-1.0, raytrace_type=mode), 96, 54, None, ex))
+    return out
+
+
 def scene_for(kind, sizes, mx):
+    if kind == "features":
+        return sc.scene_features()
     if kind == "bh":
         s = sc.scene_black_hole_only()
     else:
@@ -422,24 +474,42 @@ def scene_for(kind, sizes, mx):
     return s
 
 
+def texture_set(kind):
+    """(skybox, texture array, sizes, max size) of a golden case's texture kind."""
+    bg = sc.skybox(SKYBOX_W, SKYBOX_H)
+    if kind == "features":
+        arr, sizes, mx = sc.feature_texture_array()
+    else:
+        arr, sizes, mx = sc.default_texture_array()
+    return bg, arr, sizes, mx
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=str(Path(__file__).resolve().parent / "golden.npz"))
+    ap.add_argument("--set", choices=["r1", "r2"], default="r1",
+                    help="r1: golden.npz (round-1 cases); r2: golden_r2.npz (reseed, config 2, material flags)")
+    ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None)
     args = ap.parse_args(argv)
+    out_path = args.out or str(Path(__file__).resolve().parent / ("golden.npz" if args.set == "r1" else "golden_r2.npz"))
     ss = SwiftShader()
     print("renderer:", ss.renderer)
-    bg, arr, sizes, mx = textures()
-    ss.set_textures(bg, arr)
     store = {"meta_renderer": np.frombuffer(ss.renderer.encode(), dtype=np.uint8),
              "meta_skybox_shape": np.array([SKYBOX_H, SKYBOX_W], dtype=np.int32)}
     names = []
-    for name, kind, cam, params, W, H, tr, extras in cases():
+    bound = None
+    for name, kind, cam, params, W, H, tr, extras in (cases() if args.set == "r1" else cases_r2()):
         if args.only and name != args.only:
             continue
+        tex_kind = extras.get("textures", "default")
+        bg, arr, sizes, mx = texture_set(tex_kind)
+        if bound != tex_kind:
+            ss.set_textures(bg, arr)
+            bound = tex_kind
+        profile = extras.get("profile", "default")
         scene = scene_for(kind, sizes, mx)
         t0 = time.time()
-        img = ss.render(scene, cam, params, W, H, tr)
+        img = ss.render(scene, cam, params, W, H, tr, profile=profile)
         dt = time.time() - t0
         store[f"{name}/rgba8"] = img
         store[f"{name}/scene"] = sc.struct_bytes(scene)
@@ -447,19 +517,21 @@ def main(argv=None):
         store[f"{name}/params"] = sc.struct_bytes(params)
         store[f"{name}/size"] = np.array([W, H], dtype=np.int32)
         store[f"{name}/test_ray"] = sc.struct_bytes(tr if tr is not None else abi.default_test_ray())
+        if tex_kind != "default":
+            store[f"{name}/textures"] = np.frombuffer(tex_kind.encode(), dtype=np.uint8)
         msg = f"{name:22s} {W}x{H} steps={params.max_steps} {dt:6.2f}s"
         if extras.get("steps"):
-            st = ss.render(scene, cam, params, W, H, tr, steps_variant=True)
+            st = ss.render(scene, cam, params, W, H, tr, steps_variant=True, profile=profile)
             steps = st[:, :, 0].astype(np.int32) + 256 * st[:, :, 1].astype(np.int32)
             store[f"{name}/steps"] = steps.astype(np.uint16)
             msg += f" mean_steps={steps.mean():.1f}"
         if extras.get("float"):
-            store[f"{name}/rgba32"] = ss.render(scene, cam, params, W, H, tr, float_target=True)
+            store[f"{name}/rgba32"] = ss.render(scene, cam, params, W, H, tr, float_target=True, profile=profile)
         names.append(name)
         print(msg, flush=True)
     store["meta_cases"] = np.frombuffer("\n".join(names).encode(), dtype=np.uint8)
-    np.savez_compressed(args.out, **store)
-    print("wrote", args.out, Path(args.out).stat().st_size, "bytes")
+    np.savez_compressed(out_path, **store)
+    print("wrote", out_path, Path(out_path).stat().st_size, "bytes")
 
 
 if __name__ == "__main__":

