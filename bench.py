@@ -4,13 +4,21 @@ scene (BASELINE.json `metric`, config 3), curved mode, noise mask off.
 
 One step = one full frame: every rank renders its block-cyclic share of the
 frame's rows (8-row blocks, block b -> rank b % N) with the gfx950 kernel,
-then the tiles are gathered to rank 0 over RCCL (torch.distributed "nccl").
-`value` = frame pixels x K / (max over ranks of the timed span) — strong
+then the tiles are gathered to rank 0 (RCCL over xGMI with the default
+"nccl" backend; "gloo" stages the tiles through host memory, which lets N
+ranks share one GPU for a functional rehearsal of the distributed path).
+`value` = frame pixels x K / (max over ranks of the timed span) - strong
 scaling (the frame is fixed, the GPUs share it).
 
-Inputs are resident in HBM before timing (scene, textures, step table).
-Also reported: the kernel's roofline (algorithmic FLOP/s from the executed
-step count, SURVEY §8d cost model, HIP events on the render stream) and the
+Inputs are resident in HBM before timing: the scene, the step table and the
+reference's own textures (assets/textures: 2k skybox, 8k for the 7680x4320
+still, uv_checker + cubemap array) unless --textures standin. The camera is
+the app's default one, or the app's H-key flyby (--camera flyby: a new
+hyperbolicTrajectory camera every frame).
+
+Also reported (rank 0): the integrate kernel's roofline - executed FP32 FLOP
+per launch from rocprofv3 counters (profiles/pmc_latest.json, matched to this
+kernel source and config) over the same timed run's frame time - and the
 reference's CPU press-R geodesic loop swept over a sample of the frame's
 pixels on this host (cpu_baseline; oracle restatement, "port").
 
@@ -20,8 +28,10 @@ pixels on this host (cpu_baseline; oracle restatement, "port").
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -29,17 +39,21 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-# algorithmic cost per executed chord step in the default
-# scene (integrator 71 + black hole 17 + six objects, all-miss) and per pixel.
+KERNEL_SRC = ROOT / "schwarzschild-raytracer_amd" / "csrc" / "kernels" / "geodesic.hip"
+# the reference loop's cost per executed chord step in the
+# default scene (integrator 71 + black hole 17 + six objects, all-miss) and
+# per pixel - what the un-culled shader would execute, kept for reference.
 FLOP_PER_STEP = 360.0
 FLOP_PER_PIXEL = 150.0
-FLOP_PER_PIXEL_INTEGRATE = 100.0  # ray generation (P3, ~40) + orbital seed (P6, ~60); lighting is the shade kernel's
-# MI355X_MICROARCH.md: FP32 vector peak (packed FMA) and HBM3E peak.
+# MI355X_MICROARCH.md: FP32 vector peak (1024 SIMDs x 2.4 GHz x 64 FLOP/cycle:
+# one wave64 v_fma_f32 per 2 cycles) and HBM3E peak.
 PEAK_FP32_TFLOPS = 157.3
-PEAK_FP32_UNPACKED_TFLOPS = 78.6
 PEAK_HBM_GBS = 8000.0
+CLOCK_GHZ = 2.4
+SIMDS = 1024
 BLOCK_ROWS = 8
 CRITICAL_CANDIDATES = 8  # 16-row bands timed alone for roofline.critical_path
+MAX_HW_QUEUES = 32  # gpurun's cap on GPU_MAX_HW_QUEUES
 # BASELINE.json configs: name -> (width, height, max_steps)
 WORKLOADS = {
     "small": (640, 360, 1000),       # config 2
@@ -48,12 +62,23 @@ WORKLOADS = {
     "8k": (7680, 4320, 8000),        # config 5 (offline still)
 }
 MODES = {"curved": 0, "flat": 1, "half_width": 2, "half_height": 3}
+FLYBY = (30.0, 10.0)  # src/main.cpp:409: hyperbolicTrajectory(30, 10, t)
 
 
 def frames_in_flight(width, height, world):
     """Default frames in flight per GPU: 4 while a rank holds at least a
     quarter of a 1080p frame, 6 below that."""
     return 4 if width * height / world >= 1920 * 1080 / 4 else 6
+
+
+def hw_queues_needed(frames, world, backend):
+    """Hardware queues a rank wants: one per in-flight frame's stream, plus
+    the collective's internal streams (RCCL) and the default stream."""
+    return frames + (2 if world > 1 and backend == "nccl" else 0) + 1
+
+
+def kernel_sha() -> str:
+    return hashlib.sha256(KERNEL_SRC.read_bytes()).hexdigest()[:16]
 
 
 def parse():
@@ -71,13 +96,31 @@ def parse():
     ap.add_argument("--curved-percentage", type=float, default=0.5)
     ap.add_argument("--percent-black", type=float, default=-1.0,
                     help="noise mask (frag:839-841, 879); the app runs 0.75, the headline -1 (off)")
+    ap.add_argument("--camera", choices=["static", "flyby"], default="static",
+                    help="static: the app's default camera; flyby: the H-key hyperbolic trajectory, a new camera "
+                         "every frame (src/main.cpp:404-410)")
+    ap.add_argument("--textures", choices=["auto", "assets", "standin"], default="auto",
+                    help="assets: the reference's own textures (assets/textures); standin: procedural ones of the "
+                         "same shapes; auto: assets when present")
+    ap.add_argument("--skybox", choices=["auto", "2k", "8k"], default="auto",
+                    help="BACKGROUND_TEXTURE_QUALITY (src/main.cpp:57-63); auto: 8k for the 8k still, else 2k")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU, each on its own context and stream (0: 4, or 6 when the rank holds under a quarter of a 1080p frame)")
+                    help="frames in flight per GPU, each on its own context and stream (0: 4, or 6 when the rank "
+                         "holds under a quarter of a 1080p frame)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl: RCCL gather of device tiles over xGMI (one GPU per rank); gloo: tiles staged "
+                         "through host memory (ranks may share a GPU)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--critical-path", choices=["on", "off"], default="on",
-                    help="time the slowest row bands alone (extra launches of the same kernel; off for rocprof stats)")
+                    help="time the slowest row bands alone (extra launches of the same kernel; off for rocprof)")
+    ap.add_argument("--reference-loop", choices=["on", "off"], default="on",
+                    help="time one un-culled frame (the reference's per-step all-object loop) for "
+                         "roofline.speedup_vs_reference_loop")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
+    ap.add_argument("--dump-frames", default="",
+                    help="directory: rank 0 saves every timed frame as assembled (frame_<f>.npy), for the "
+                         "multi-rank parity test; copies are taken after the timed region")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
     ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
     return ap.parse_args()
@@ -85,10 +128,25 @@ def parse():
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    W0, H0, N0 = WORKLOADS[args.workload]
+    W, H, N = args.width or W0, args.height or H0, args.max_steps or N0
+    F = args.inflight if args.inflight > 0 else frames_in_flight(W, H, world)
     # every in-flight frame's stream needs a hardware queue of its own (HIP's
-    # default is 4 per process); must be set before the HIP runtime starts
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+    # default is 4 per process); must be set before the HIP runtime starts.
+    # Under a profiler whose preloaded library has already started HIP the
+    # in-process value is ignored: set it on the command line there.
+    need = hw_queues_needed(F, world, args.dist_backend)
+    if need > MAX_HW_QUEUES:
+        F = MAX_HW_QUEUES - (need - F)
+        print(f"bench: clamping frames in flight to {F} ({MAX_HW_QUEUES} hardware queues)", file=sys.stderr)
+        need = MAX_HW_QUEUES
+    have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    if have < need:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(need)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -97,67 +155,92 @@ def main():
 
     pkg = srpkg.load_package()
     abi, sc = pkg.abi, pkg.scenes
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    ndev = max(1, torch.cuda.device_count())
+    dev = torch.device("cuda", local % ndev)
     if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    W0, H0, N0 = WORKLOADS[args.workload]
-    W, H, N = args.width or W0, args.height or H0, args.max_steps or N0
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(dev)
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     # ---- inputs resident in HBM ---------------------------------------------------
     scene = sc.scene_default(textured=True)
-    cam = abi.default_camera()
     params = abi.default_params(max_steps=N, percent_black=args.percent_black, raytrace_type=MODES[args.mode],
                                 curved_percentage=args.curved_percentage)
+    quality = args.skybox if args.skybox != "auto" else ("8k" if (W, H) == WORKLOADS["8k"][:2] else "2k")
+    use_assets = args.textures == "assets" or (args.textures == "auto" and pkg.assets.available())
+    if use_assets:
+        skybox = pkg.assets.skybox(quality)
+        arr, _, _ = pkg.assets.texture_array()
+    else:
+        skybox = sc.skybox(*((8192, 4096) if quality == "8k" else (2048, 1024)))
+        arr, _, _ = sc.default_texture_array()
+    # Cameras: frame f of the run (warmup + timed) uses cams[f].
+    n_frames = max(args.warmup, F) + args.steps
+    if args.camera == "flyby":
+        cams = [abi.camera_flyby((f + 0.5) / n_frames, *FLYBY) for f in range(n_frames)]
+    else:
+        cams = [abi.default_camera()] * n_frames
     # Frames in flight: a frame's time is bounded by the latency of its
     # longest rays' waves, which a share of 1/N of the rows
     # does not shorten; independent frames on their own contexts and streams
-    # fill the SIMDs those waves leave idle. Step f renders frame f on context
-    # f % F and gathers it to rank 0 on that context's stream.
-    # (measured with tools/inflight.py --shard, profiles/r01/s12_inflight_shards.txt:
-    # one rank's share of an 8-GPU frame takes 1.60 ms alone, 0.34 ms per frame
-    # with 6 in flight; of a 2-GPU frame 0.83 ms with 2, 0.76 ms with 4).
-    # What matters is the rank's pixel count: 4 in flight while a rank holds at
-    # least a quarter of a 1080p frame, 6 below that (an 8-GPU share, config 2).
-    # Re-measured at N = 1 (profiles/r01/s18_inflight_headline.jsonl): 2 / 3 /
-    # 4 / 6 in flight give 1.44 / 1.41 / 1.41 / 1.41 ms per frame.
-    F = args.inflight if args.inflight > 0 else frames_in_flight(W, H, world)
-    skybox = sc.skybox(2048, 1024)
-    arr, _, _ = sc.default_texture_array()
+    # fill the SIMDs those waves leave idle. Frame f renders on context f % F
+    # and is gathered to rank 0 on that context's stream (nccl), or through
+    # host memory once it is done (gloo).
     D = pkg.dist
+    gloo = distributed and args.dist_backend == "gloo"
     ctxs = []
     for k in range(F):
-        rk = pkg.Renderer(local)
+        rk = pkg.Renderer(dev.index)
         rk.set_scene(scene)
         rk.set_background(skybox)
         rk.set_texture_array(arr)
         rk.set_culling(not args.no_cull)
         tile_k = torch.zeros((D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
-        ctxs.append((rk, tile_k, D.FrameGather(tile_k, world, rank, H, BLOCK_ROWS),
-                     torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)))
-    r, tile, gather, stream = ctxs[0]
+        host_k = torch.zeros(tuple(tile_k.shape), dtype=torch.uint8).pin_memory() if gloo else None
+        gather_k = D.FrameGather(host_k if gloo else tile_k, world, rank, H, BLOCK_ROWS)
+        ctxs.append((rk, tile_k, gather_k, torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev),
+                     host_k))
+    r, tile, _, stream, _ = ctxs[0]
 
-    def render_tile():
-        r.render_blocks(cam, params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+    frames = {}  # --dump-frames: frame index -> assembled frame (rank 0), timed frames only
+    dump_from = [1 << 30]
 
-    def step(f=0):
-        rk, tile_k, gather_k, s_k = ctxs[f % F]
+    def keep(f, frame):
+        if args.dump_frames and frame is not None and f >= dump_from[0]:
+            frames[f] = frame.clone()  # on the frame's stream (nccl) or host (gloo)
+
+    def launch(f):
+        rk, tile_k, gather_k, s_k, host_k = ctxs[f % F]
         with torch.cuda.stream(s_k):
-            rk.render_blocks(cam, params, W, H, BLOCK_ROWS, rank, world, out=tile_k, stream=s_k)
-            return gather_k()  # the assembled frame on rank 0 (RCCL gather for N > 1)
+            rk.render_blocks(cams[f], params, W, H, BLOCK_ROWS, rank, world, out=tile_k, stream=s_k)
+            if gloo:
+                host_k.copy_(tile_k, non_blocking=True)
+                return
+            keep(f, gather_k())  # the assembled frame on rank 0 (RCCL gather for N > 1)
+
+    def complete(f):  # gloo: the frame's host tile is gathered once its render is done
+        if gloo:
+            _, _, gather_k, s_k, _ = ctxs[f % F]
+            s_k.synchronize()
+            keep(f, gather_k())
+
+    def run_frames(first, count):
+        for f in range(first, first + count):
+            launch(f)
+            if f - first >= F - 1:
+                complete(f - F + 1)
+        for f in range(max(first, first + count - F + 1), first + count):
+            complete(f)
 
     def sync_all():
-        for _, _, _, s_k in ctxs:
-            s_k.synchronize()
+        for c in ctxs:
+            c[3].synchronize()
 
     # executed steps of this rank's rows (untimed; the debug variant of the kernel)
     rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
-    _, _, steps_full = r.render_debug(cam, params, W, H)
+    _, _, steps_full = r.render_debug(cams[0], params, W, H)
     torch.cuda.synchronize(dev)
     sigma_steps_frame = int(steps_full.sum().item())
     sigma_steps_mine = int(steps_full[rows_mine].sum().item())
@@ -167,46 +250,69 @@ def main():
     band_rows = [int(b) * 16 for b in band_max.argsort(descending=True)[:CRITICAL_CANDIDATES].tolist()] or [0]
     del steps_full, band_max
 
-    for f in range(max(args.warmup, F)):  # every context learns its launch order
-        step(f)
+    warm = max(args.warmup, F)  # every context learns its launch order
+    run_frames(0, warm)
     sync_all()
 
-    # kernel-only timing with HIP events on the render stream (separate loop
-    # so the gather does not sit between the events); the library records
-    # per-kernel events (integrate / shade / resume) for the same frames
-    r.set_timing(args.steps)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(stream)
-    for _ in range(args.steps):
-        render_tile()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    ktimes = r.kernel_times(args.steps)
-    r.set_timing(0)
-    integrate_ms, shade_ms, resume_ms = (float(x) for x in ktimes.mean(axis=0))
-
+    # ---- the timed region: K frames, F in flight, per-kernel HIP events on
+    # every context's stream (integrate / shade / resume of each frame)
+    per_ctx = -(-args.steps // F) + 1
+    dump_from[0] = warm
+    for c in ctxs:
+        c[0].set_timing(per_ctx)
     if distributed:
         dist.barrier()
     sync_all()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for f in range(args.steps):
-        step(f)
+    run_frames(warm, args.steps)
     sync_all()
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    ktimes = np.concatenate([c[0].kernel_times(per_ctx) for c in ctxs], axis=0)
+    if args.dump_frames and rank == 0:
+        Path(args.dump_frames).mkdir(parents=True, exist_ok=True)
+        for f, fr in frames.items():
+            np.save(Path(args.dump_frames) / f"frame_{f}.npy", fr.cpu().numpy())
+        frames.clear()
+    for c in ctxs:
+        c[0].set_timing(0)
+    integrate_ms, shade_ms, resume_ms = (float(x) for x in ktimes.mean(axis=0))
+
+    # single-frame latency (untimed for `value`): one frame alone on context 0
+    lat_frames = 5
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for f in range(lat_frames):
+        r.render_blocks(cams[warm + f % args.steps], params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    latency_ms = ev0.elapsed_time(ev1) / lat_frames
+
+    # the reference's loop: one un-culled frame against one culled frame, alone
+    speedup_ref = None
+    if args.reference_loop == "on" and not args.no_cull and rank == 0:
+        def alone_integrate_ms(cull):
+            r.set_culling(cull)
+            r.set_timing(2)
+            for _ in range(2):
+                r.render_blocks(cams[0], params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+            torch.cuda.synchronize(dev)
+            t = float(r.kernel_times(2)[-1, 0])
+            r.set_timing(0)
+            return t
+        culled = alone_integrate_ms(True)
+        unculled = alone_integrate_ms(False)
+        r.set_culling(True)
+        speedup_ref = {"culled_ms": round(culled, 4), "reference_loop_ms": round(unculled, 4),
+                       "speedup": round(unculled / culled, 2)}
+
+    if distributed:  # max over ranks (RCCL reduces device tensors, gloo host ones)
+        t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=None if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        k = torch.tensor([kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(k, op=dist.ReduceOp.MAX)
-        kernel_ms_max = float(k.item())
-    else:
-        kernel_ms_max = kernel_ms
+        elapsed, latency_ms = float(t[0]), float(t[1])
 
     ms_per_step = elapsed * 1e3 / args.steps
     mpix_s = W * H * args.steps / elapsed / 1e6
@@ -217,7 +323,7 @@ def main():
     # slowest waves' latency without contention.
     critical = None
     if rank == 0 and world == 1 and args.critical_path == "on":
-        rb = pkg.Renderer(local)
+        rb = pkg.Renderer(dev.index)
         rb.set_scene(scene)
         rb.set_background(skybox)
         rb.set_texture_array(arr)
@@ -225,12 +331,12 @@ def main():
 
         def band_time(band, reps):
             for _ in range(2):
-                rb.render(cam, params, W, H, *band, stream=stream)
+                rb.render(cams[0], params, W, H, *band, stream=stream)
             times = []
             for _ in range(reps):
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
-                rb.render(cam, params, W, H, *band, stream=stream)
+                rb.render(cams[0], params, W, H, *band, stream=stream)
                 e1.record(stream)
                 torch.cuda.synchronize(dev)
                 times.append(e0.elapsed_time(e1))
@@ -243,72 +349,17 @@ def main():
         band_ms = band_time(band, 5)
         rb.close()
         critical = {"band_rows": list(band), "band_ms": round(band_ms, 4),
-                    "frac_of_frame": round(band_ms / kernel_ms, 3)}
+                    "frac_of_frame_latency": round(band_ms / latency_ms, 3)}
 
     if rank == 0:
-        # roofline of the dominant kernel (sr_integrate_kernel: ray generation,
-        # the step loop and every intersection test), on rank 0's launch
-        flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL_INTEGRATE
-        achieved_tflops = flop / (integrate_ms * 1e-3) / 1e12
-        frame_flop = sigma_steps_mine * FLOP_PER_STEP + len(rows_mine) * W * FLOP_PER_PIXEL
-        hbm_bytes = len(rows_mine) * W * 4  # compulsory RGBA8 store; textures stay cache resident
-        traffic = None
-        tj = Path(args.traffic_json)
-        if tj.exists():
-            try:
-                rec = json.loads(tj.read_text())
-                if rec.get("width") == W and rec.get("height") == H and rec.get("max_steps") == N and world == 1:
-                    traffic = rec.get("hbm_bytes_per_launch")
-            except Exception:  # noqa: BLE001
-                traffic = None
-        pmc = None
-        pj = Path(args.pmc_json)
-        if pj.exists():
-            try:
-                rec = json.loads(pj.read_text())
-                if rec.get("width") == W and rec.get("height") == H and rec.get("max_steps") == N and world == 1:
-                    pmc = {k: rec[k] for k in ("valu_busy", "salu_per_valu", "source") if k in rec}
-            except Exception:  # noqa: BLE001
-                pmc = None
-        roofline = {
-            "bound": "valu",
-            "kernel": "sr_integrate_kernel",
-            "achieved": round(achieved_tflops, 3),
-            "peak": PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tflops / PEAK_FP32_TFLOPS, 4),
-            "traffic": traffic,
-            "frac_unpacked_peak": round(achieved_tflops / PEAK_FP32_UNPACKED_TFLOPS, 4),
-            "kernel_ms": round(integrate_ms, 4),
-            "flop_per_launch": flop,
-            "steps_per_launch": sigma_steps_mine,
-            "mean_steps_per_pixel": round(sigma_steps_frame / (W * H), 2),
-            "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
-                            "resume": round(resume_ms, 4), "frame_events": round(kernel_ms, 4)},
-            "frame": {
-                "achieved": round(frame_flop / (kernel_ms * 1e-3) / 1e12, 3),
-                "unit": "TFLOP/s",
-                "flop_per_frame": frame_flop,
-                "frac": round(frame_flop / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS, 4),
-            },
-            # algorithmic = the reference loop's work; culling
-            # executes a fraction of it, so frac can approach or pass 1. The
-            # frame is bounded by the latency of its longest rays' waves:
-            # critical_path = their band alone; pmc = executed VALU issue
-            # (profiles/pmc_latest.json, same config)
-            "critical_path": critical,
-            "pmc": pmc,
-            "hbm": {
-                "achieved": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9, 3),
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": round(hbm_bytes / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
-                "algorithmic_bytes": hbm_bytes,
-            },
-        }
+        roofline = make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, resume_ms,
+                                 latency_ms, sigma_steps_frame, sigma_steps_mine, len(rows_mine), critical,
+                                 speedup_ref)
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
-            cpu = cpu_baseline(cam, W, H, N, args.cpu_sample_rows)
+            cpu = cpu_baseline(cams[0], W, H, N, args.cpu_sample_rows)
+        tex_desc = (f"the reference's assets/textures ({quality} skybox, uv_checker, cubemap; PIL-decoded)"
+                    if use_assets else f"procedural stand-in textures ({quality} skybox)")
         line = {
             "metric": ("Mpixels/s at 1920x1080, 2000 geodesic steps; 1/2/4/8 MI355X"
                        if (W, H, N) == WORKLOADS["headline"] else f"Mpixels/s at {W}x{H}, {N} geodesic steps"),
@@ -322,20 +373,26 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (default scene of src/main.cpp:222-268, procedural stand-in textures)",
+            "data": f"synthetic: default scene of src/main.cpp:222-268, {tex_desc}",
             "config": {
                 "workload": (f"{W}x{H} {args.mode}-mode frame"
                              + (f" (curved_percentage {args.curved_percentage})" if args.mode.startswith("half") else "")
                              + f", {N} geodesic steps, default scene, percent_black "
-                             + ("off" if args.percent_black < 0 else str(args.percent_black))),
+                             + ("off" if args.percent_black < 0 else str(args.percent_black))
+                             + (", flyby camera (a new camera every frame)" if args.camera == "flyby" else "")),
                 "width": W,
                 "height": H,
                 "max_steps": N,
-                "tiling": f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), RCCL gather to rank 0",
+                "camera": args.camera,
+                "textures": "assets" if use_assets else "standin",
+                "skybox": quality,
+                "tiling": (f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), "
+                           + ("RCCL gather to rank 0" if not gloo else "gloo gather of host-staged tiles to rank 0")),
+                "dist_backend": args.dist_backend if distributed else None,
                 "frames_in_flight": F,
-                "frame_latency_ms": round(kernel_ms_max, 4),
+                "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                "frame_latency_ms": round(latency_ms, 4),
                 "culling": not args.no_cull,
-                "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -344,37 +401,162 @@ def main():
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
-    for rk, _, _, _ in ctxs:
-        rk.close()
+    for c in ctxs:
+        c[0].close()
+
+
+def load_matching(path, W, H, N, world):
+    """A profiles/*.json record if it was measured on this config and kernel source."""
+    p = Path(path)
+    if not p.exists():
+        return None
+    try:
+        rec = json.loads(p.read_text())
+    except Exception:  # noqa: BLE001
+        return None
+    if (rec.get("width"), rec.get("height"), rec.get("max_steps")) != (W, H, N):
+        return None
+    if rec.get("kernel_sha") not in (None, kernel_sha()):
+        return None
+    return rec
+
+
+def make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, resume_ms, latency_ms,
+                  sigma_steps_frame, sigma_steps_mine, rows_mine, critical, speedup_ref):
+    """Roofline of the dominant kernel (sr_integrate_kernel: ray generation,
+    the step loop and every intersection test), on rank 0's launches.
+
+    The path is FP32-VALU bound (no contraction for MFMA, ~4 B of compulsory
+    HBM traffic per pixel). `achieved` is the FP32 work the kernel EXECUTES:
+    the FLOP per launch counted by the hardware (SQ_INSTS_VALU_FLOPS_FP32 +
+    _TRANS, rocprofv3 --pmc on this kernel source and config, calibrated by
+    tools/microbench/flops_calib.hip: profiles/pmc_latest.json) times the
+    launches per second of this run (one per frame, F in flight), so `frac`
+    is utilisation of the FP32 peak. `kernel_ms` is the same run's mean
+    integrate-launch duration (HIP events on each frame's stream; launches
+    overlap F-fold, `overlap` = kernel_ms / ms_per_step): it is what the
+    rocprofv3 --stats summary of this command reports."""
+    pmc = load_matching(args.pmc_json, W, H, N, world)
+    share = sigma_steps_mine / max(1, sigma_steps_frame)  # rank 0's share of the frame's steps
+    executed = None
+    achieved = None
+    valu_issue = None
+    if pmc and pmc.get("flop_per_launch"):
+        executed = pmc["flop_per_launch"] * share
+        achieved = executed / (ms_per_step * 1e-3) / 1e12
+        if pmc.get("valu_insts_per_launch"):
+            # wave64 VALU instructions x 2 cycles on a SIMD-32 over the SIMD-cycles at 2.4 GHz
+            valu_issue = pmc["valu_insts_per_launch"] * share * 2.0 / (SIMDS * CLOCK_GHZ * 1e9 * ms_per_step * 1e-3)
+    traffic = None
+    tr = load_matching(args.traffic_json, W, H, N, world)
+    if tr and world == 1:
+        traffic = tr.get("hbm_bytes_per_launch")
+    hbm_bytes = rows_mine * W * 4  # compulsory RGBA8 store; textures stay cache resident
+    ref_flop = sigma_steps_mine * FLOP_PER_STEP + rows_mine * W * FLOP_PER_PIXEL
+    return {
+        "bound": "valu",
+        "kernel": "sr_integrate_kernel",
+        "achieved": None if achieved is None else round(achieved, 3),
+        "peak": PEAK_FP32_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": None if achieved is None else round(achieved / PEAK_FP32_TFLOPS, 4),
+        "traffic": traffic,
+        "executed_flop_per_launch": None if executed is None else round(executed),
+        "valu_issue_frac": None if valu_issue is None else round(valu_issue, 4),
+        "kernel_ms": round(integrate_ms, 4),
+        "overlap": round(integrate_ms / ms_per_step, 2),
+        "frames_in_flight": F,
+        "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
+                        "resume": round(resume_ms, 4)},
+        "steps_per_launch": sigma_steps_mine,
+        "mean_steps_per_pixel": round(sigma_steps_frame / (W * H), 2),
+        "pmc_source": None if not pmc else pmc.get("source"),
+        # the un-culled reference loop (SURVEY §8d: 360 FLOP per step) and the
+        # measured speed-up of the culled kernel over it; not utilisation
+        "reference_loop": {"flop_per_frame": ref_flop, **(speedup_ref or {})},
+        "critical_path": critical,
+        "hbm": {
+            "achieved": round(hbm_bytes / (ms_per_step * 1e-3) / 1e9, 3),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(hbm_bytes / (ms_per_step * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
+            "algorithmic_bytes": hbm_bytes,
+        },
+    }
+
+
+def host_cpu():
+    """(threads to use, nproc, CPU model): the box's CPU share is what
+    OMP_NUM_THREADS says there (16 per GPU); nproc counts the whole machine."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = min(aff, share) if share > 0 else aff
+    model = "unknown"
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:  # noqa: BLE001
+        pass
+    return threads, nproc, model
 
 
 def cpu_baseline(cam, W, H, N, sample_rows):
     """The reference's press-R CPU geodesic (src/main.cpp:73-124) swept over
-    a bounded sample of the frame's pixels, all host cores (oracle port)."""
+    a bounded sample of the frame's pixels: all threads of
+    this host's CPU share, -O2 (official) and -O0 (the reference's CMake
+    default), median of 3 runs each (oracle port)."""
+    import statistics
+
     import srpkg
 
     oracle = srpkg.load_oracle()
-    threads = min(16, os.cpu_count() or 1)
+    threads, nproc, model = host_cpu()
     if sample_rows <= 0:
-        # calibrate: time 8 rows, size the sample to ~10 s of work
+        # calibrate: time 8 rows, size the sample to ~3 s per -O2 run
         t = time.perf_counter()
         oracle.pressr_sweep(cam, W, H, N, 2, H // 2 - 4, H // 2 + 4, threads)
         dt = max(time.perf_counter() - t, 1e-3)
-        sample_rows = int(min(H, max(8, 8 * 10.0 / dt)))
-    # evenly spread bands: rows [y0, y0 + n) around the frame centre
-    y0 = max(0, H // 2 - sample_rows // 2)
-    y1 = min(H, y0 + sample_rows)
-    t = time.perf_counter()
-    pts = oracle.pressr_sweep(cam, W, H, N, 2, y0, y1, threads)
-    dt = time.perf_counter() - t
-    px = (y1 - y0) * W
+        sample_rows = int(min(H, max(8, 8 * 3.0 / dt)))
+
+    def rate(fn, rows):
+        y0 = max(0, H // 2 - rows // 2)  # rows [y0, y1) around the frame centre
+        y1 = min(H, y0 + rows)
+        runs = []
+        pts = 0
+        for _ in range(3):
+            t = time.perf_counter()
+            pts = fn(cam, W, H, N, 2, y0, y1, threads)
+            runs.append(time.perf_counter() - t)
+        dt = statistics.median(runs)
+        return (y1 - y0) * W / dt / 1e6, y0, y1, pts, dt
+
+    v2, y0, y1, pts, dt = rate(oracle.pressr_sweep, sample_rows)
+    o0 = None
+    if hasattr(oracle, "pressr_sweep_O0"):
+        try:
+            rows0 = max(8, sample_rows // 4)
+            v0, a0, b0, _, d0 = rate(oracle.pressr_sweep_O0, rows0)
+            o0 = {"value": round(v0, 4), "sample": f"rows [{a0},{b0}) x {W} px, median {d0:.2f} s"}
+        except (FileNotFoundError, OSError):
+            o0 = None
     return {
-        "value": round(px / dt / 1e6, 4),
+        "value": round(v2, 4),
         "unit": "Mpixels/s",
         "cores": threads,
         "kind": "port",
         "sample": f"press-R loop (src/main.cpp:73-124) over rows [{y0},{y1}) x {W} px of the {W}x{H} frame, "
-                  f"{N} steps, {pts} points, {dt:.2f} s, -O2",
+                  f"{N} steps, {pts} points, median of 3 runs {dt:.2f} s, -O2, {threads} threads",
+        "nproc": nproc,
+        "cpu_model": model,
+        "O0": o0,
+        "note": "integrator only: the press-R loop does no scene intersection or shading (BASELINE.md §3)",
     }
 
 

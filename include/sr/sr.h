@@ -240,6 +240,13 @@ void sr_scene_clear(sr_scene* out);
  * described by texture_sizes (uv_checker 600x600, cubemap 1601x1201). */
 void sr_default_scene(sr_scene* out);
 void sr_default_camera(sr_camera* out);
+/* The app's H-key flyby (src/main.cpp:404-410 -> Camera::hyperbolicTrajectory,
+ * camera.cpp:20-33, then lookAt(origin), camera.cpp:35-39): moves *cam along
+ * the hyperbola of the given initial / closest distance at eased time t in
+ * [0, 1] (the app: 30, 10, elapsed / HYPERBOLIC_TRAJECTORY_DURATION). The fov
+ * is kept. Host-only, per frame. */
+int sr_camera_hyperbolic_trajectory(sr_camera* cam, float initial_distance, float closest_distance,
+                                    float time);
 
 /* Context ------------------------------------------------------------------- */
 int sr_create(sr_ctx** out, int hip_device);

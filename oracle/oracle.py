@@ -15,6 +15,7 @@ import srpkg
 abi = srpkg.load_package().abi
 
 LIB_PATH = Path(__file__).resolve().parent / "build" / "libsr_oracle.so"
+LIB_O0_PATH = Path(__file__).resolve().parent / "build" / "libsr_oracle_O0.so"  # bench cpu_baseline -O0 leg
 
 
 class Textures(C.Structure):
@@ -110,6 +111,25 @@ def test_ray_points(pos, forward, max_steps, max_revolutions=2):
     n = lib.sro_test_ray_points((C.c_float * 3)(*pos), (C.c_float * 3)(*forward), max_steps, max_revolutions,
                                 buf, cap)
     return [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(min(n, cap))]
+
+
+_lib_O0 = None
+
+
+def pressr_sweep_O0(cam, width, height, max_steps, max_revolutions=2, row_begin=0, row_end=None, nthreads=0) -> int:
+    """pressr_sweep built at -O0 (the reference's CMake default)."""
+    global _lib_O0
+    if _lib_O0 is None:
+        if not LIB_O0_PATH.exists():
+            raise FileNotFoundError(f"{LIB_O0_PATH} not built; run make -C oracle")
+        lib = C.CDLL(str(LIB_O0_PATH))
+        lib.sro_pressr_sweep.restype = C.c_int64
+        lib.sro_pressr_sweep.argtypes = [C.POINTER(abi.Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_int]
+        _lib_O0 = lib
+    row_end = height if row_end is None else row_end
+    return int(_lib_O0.sro_pressr_sweep(C.byref(cam), width, height, row_begin, row_end, max_steps, max_revolutions,
+                                        nthreads))
 
 
 def pressr_sweep(cam, width, height, max_steps, max_revolutions=2, row_begin=0, row_end=None, nthreads=0) -> int:

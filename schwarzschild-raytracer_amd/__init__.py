@@ -9,14 +9,15 @@ Layout:
   abi.py                     ctypes mirror of sr.h
   renderer.py                Renderer: device handle (torch for memory/streams)
   scenes.py                  scenes, cameras, stand-in textures
+  assets.py                  the reference's own textures (assets/textures) decoded as stb_image does
   dist.py                    row-band tiling over ranks + RCCL gather
 
 Import as a package via `load_package()` in bench.py / tests (the directory
 name is not a Python identifier).
 """
-from . import abi, dist, scenes  # noqa: F401
+from . import abi, assets, dist, scenes  # noqa: F401
 
-__all__ = ["abi", "dist", "scenes", "Renderer"]
+__all__ = ["abi", "assets", "dist", "scenes", "Renderer"]
 
 
 def __getattr__(name):

@@ -174,6 +174,7 @@ SIGNATURES = {
     "sr_scene_clear": (None, [C.POINTER(Scene)]),
     "sr_default_scene": (None, [C.POINTER(Scene)]),
     "sr_default_camera": (None, [C.POINTER(Camera)]),
+    "sr_camera_hyperbolic_trajectory": (C.c_int, [C.POINTER(Camera), C.c_float, C.c_float, C.c_float]),
     "sr_create": (_i, [C.POINTER(_p), _i]),
     "sr_destroy": (None, [_p]),
     "sr_set_background": (_i, [_p, _p, _i, _i, _i]),
@@ -278,6 +279,18 @@ def default_scene() -> Scene:
 def default_camera() -> Camera:
     c = Camera()
     load().sr_default_camera(C.byref(c))
+    return c
+
+
+def camera_flyby(t: float, initial_distance: float = 30.0, closest_distance: float = 10.0,
+                 cam: Camera | None = None) -> Camera:
+    """The app's H-key flyby camera at eased time t in [0, 1] (src/main.cpp:404-410:
+    Camera::hyperbolicTrajectory(30, 10, t), camera.cpp:20-39)."""
+    src = cam if cam is not None else default_camera()
+    c = Camera()
+    C.memmove(C.addressof(c), C.addressof(src), C.sizeof(Camera))
+    check(load().sr_camera_hyperbolic_trajectory(C.byref(c), initial_distance, closest_distance, t),
+          "sr_camera_hyperbolic_trajectory")
     return c
 
 

@@ -431,6 +431,17 @@ void sr_default_camera(sr_camera* out) {
     d.cam.load(*out);
 }
 
+int sr_camera_hyperbolic_trajectory(sr_camera* cam, float initial_distance, float closest_distance, float time) {
+    if (!cam) return SR_E_INVALID;
+    const float* a = cam->transform.axes;
+    sr::Camera c(sr::vec3(cam->transform.pos[0], cam->transform.pos[1], cam->transform.pos[2]),
+                 sr::vec3(a[6], a[7], a[8]), sr::vec3(a[0], a[1], a[2]));
+    c.setFov(cam->fov);
+    c.hyperbolicTrajectory(initial_distance, closest_distance, time);
+    c.load(*cam);
+    return SR_OK;
+}
+
 int sr_test_ray_points(const float cam_pos[3], const float cam_forward[3], int max_steps,
                        int max_revolutions, float* out_xyz, int max_points, int* out_count) {
     if (!cam_pos || !cam_forward || max_steps < 0 || (max_points > 0 && !out_xyz))

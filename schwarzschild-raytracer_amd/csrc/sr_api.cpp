@@ -55,10 +55,19 @@ struct sr_ctx {
     int* d_count = nullptr;
     size_t ps_n = 0;
     // workgroup-tile launch order (costliest first) and per-tile cost of the
-    // last frame on this grid shape (geodesic.hip sr_order_kernel)
-    int* d_order = nullptr;
-    int* d_cost = nullptr;
-    int order_gx = 0, order_gy = 0;
+    // last frame, one pair per grid shape (geodesic.hip sr_order_kernel): kept
+    // for the context's lifetime, so a shape change never frees a buffer an
+    // in-flight frame still reads
+    struct Order {
+        int* order = nullptr;
+        int* cost = nullptr;
+    };
+    std::map<std::pair<int, int>, Order> orders;
+    // the stream of the context's last launch: a context is used from one
+    // stream, so waiting for it waits for every frame that
+    // may still read the context's buffers, and for nothing else on the device
+    hipStream_t last_stream = nullptr;
+    bool launched = false;
     // optional per-kernel timing: 4 events per frame (before integrate, after
     // integrate, after shade, after resume), a ring of `timing_cap` frames
     std::vector<hipEvent_t> tev;
@@ -343,10 +352,17 @@ void free_pixel_state(sr_ctx* ctx) {
     ctx->ps_n = 0;
 }
 
+// Waits for this context's in-flight frames (its last launch stream), not
+// for the device: other contexts' frames and collectives run on.
+bool wait_ctx(sr_ctx* ctx) {
+    if (!ctx->launched) return true;
+    return hip_ok(hipStreamSynchronize(ctx->last_stream));
+}
+
 int ensure_pixel_state(sr_ctx* ctx, size_t n) {
     if (n <= ctx->ps_n) return SR_OK;
-    // growing: wait for in-flight frames that use the old buffers
-    if (ctx->ps_n && !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    // growing: wait for this context's in-flight frames that use the old buffers
+    if (ctx->ps_n && !wait_ctx(ctx)) return SR_E_HIP;
     free_pixel_state(ctx);
     if (!hip_ok(hipMalloc(&ctx->d_ps, n * SR_PS_FIELDS * sizeof(float))) ||
         !hip_ok(hipMalloc(&ctx->d_list, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_count, 2 * sizeof(int)))) {
@@ -395,18 +411,17 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
     return SR_OK;
 }
 
-// Launch order for a new grid shape: tiles nearest the frame centre first
-// (where the black hole usually is) until a frame has measured the costs.
-int ensure_order(sr_ctx* ctx, int gx, int gy) {
-    if (ctx->order_gx == gx && ctx->order_gy == gy && ctx->d_order) return SR_OK;
-    if (ctx->order_gx || ctx->order_gy) {
-        if (!hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+// Launch order for a grid shape: tiles nearest the frame centre first (where
+// the black hole usually is) until a frame has measured the costs. One
+// buffer pair per shape, allocated on first use.
+int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
+    auto key = std::make_pair(gx, gy);
+    auto it = ctx->orders.find(key);
+    if (it != ctx->orders.end()) {
+        *order = it->second.order;
+        *cost = it->second.cost;
+        return SR_OK;
     }
-    if (ctx->d_order) (void)hipFree(ctx->d_order);
-    if (ctx->d_cost) (void)hipFree(ctx->d_cost);
-    ctx->d_order = nullptr;
-    ctx->d_cost = nullptr;
-    ctx->order_gx = ctx->order_gy = 0;
     const size_t n = (size_t)gx * gy;
     std::vector<int> ord(n);
     std::vector<double> d(n);
@@ -416,13 +431,20 @@ int ensure_order(sr_ctx* ctx, int gx, int gy) {
         d[i] = x * x + y * y;
     }
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return d[a] < d[b]; });
-    if (!hip_ok(hipMalloc(&ctx->d_order, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_cost, n * sizeof(int))))
+    sr_ctx::Order o;
+    if (!hip_ok(hipMalloc(&o.order, n * sizeof(int))) || !hip_ok(hipMalloc(&o.cost, n * sizeof(int)))) {
+        if (o.order) (void)hipFree(o.order);
         return SR_E_NOMEM;
-    if (!hip_ok(hipMemcpy(ctx->d_order, ord.data(), n * sizeof(int), hipMemcpyHostToDevice)) ||
-        !hip_ok(hipMemset(ctx->d_cost, 0, n * sizeof(int))))
+    }
+    if (!hip_ok(hipMemcpy(o.order, ord.data(), n * sizeof(int), hipMemcpyHostToDevice)) ||
+        !hip_ok(hipMemset(o.cost, 0, n * sizeof(int)))) {
+        (void)hipFree(o.order);
+        (void)hipFree(o.cost);
         return SR_E_HIP;
-    ctx->order_gx = gx;
-    ctx->order_gy = gy;
+    }
+    ctx->orders[key] = o;
+    *order = o.order;
+    *cost = o.cost;
     return SR_OK;
 }
 
@@ -478,15 +500,19 @@ int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width
     if (rc != SR_OK) return rc;
     rc = ensure_pixel_state(ctx, (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) * 256);
     if (rc != SR_OK) return rc;
+    int* order = nullptr;
+    int* cost = nullptr;
     if (nrows > 0) {
-        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16);
+        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, &order, &cost);
         if (rc != SR_OK) return rc;
     }
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
-                                      dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count,
-                                      nrows > 0 ? ctx->d_order : nullptr, nrows > 0 ? ctx->d_cost : nullptr,
+                                      dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count, order, cost,
                                       ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
-                                      reinterpret_cast<hipStream_t>(stream));
+                                      s);
+    ctx->last_stream = s;
+    ctx->launched = true;
     return hip_ok(e) ? SR_OK : SR_E_HIP;
 }
 
@@ -544,7 +570,7 @@ int sr_create(sr_ctx** out, int hip_device) {
 void sr_destroy(sr_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipDeviceSynchronize();
+    (void)wait_ctx(c);
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_segs) (void)hipFree(c->d_segs);
     if (c->d_bg) (void)hipFree(c->d_bg);
@@ -552,15 +578,17 @@ void sr_destroy(sr_ctx* c) {
     if (c->d_opq) (void)hipFree(c->d_opq);
     for (auto& kv : c->tables) (void)hipFree(kv.second.dev);
     free_pixel_state(c);
-    if (c->d_order) (void)hipFree(c->d_order);
-    if (c->d_cost) (void)hipFree(c->d_cost);
+    for (auto& kv : c->orders) {
+        (void)hipFree(kv.second.order);
+        (void)hipFree(kv.second.cost);
+    }
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     delete c;
 }
 
 int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {
     if (!c || !px || w <= 0 || h <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
-    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     int rc = upload_rgba(px, w, h, 1, ch, &c->d_bg);
     if (rc != SR_OK) {
         c->bg_w = c->bg_h = 0;
@@ -573,7 +601,7 @@ int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {
 
 int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers, int ch) {
     if (!c || !px || w <= 0 || h <= 0 || layers <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
-    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     int rc = upload_rgba(px, w, h, layers, ch, &c->d_arr);
     if (rc == SR_OK) rc = make_opacity_map(px, w, h, layers, ch, &c->d_opq);
     if (rc != SR_OK) {
@@ -662,7 +690,7 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
     std::memcpy(d.planes, s->planes, sizeof d.planes);
     std::memcpy(d.texture_sizes, s->texture_sizes, sizeof d.texture_sizes);
     std::memcpy(d.max_texture_size, s->max_texture_size, sizeof d.max_texture_size);
-    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
     c->h_scene = d;
     c->scene_set = true;
@@ -698,7 +726,7 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
         g[13] = t->radius;
     }
     d.tr_num_segments = nseg;
-    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     if (!hip_ok(hipMemcpy(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice)))
         return SR_E_HIP;
     if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
@@ -763,7 +791,7 @@ int sr_debug_set_culling(sr_ctx* c, int enabled) {
 // for its roofline line from here.
 int sr_debug_set_timing(sr_ctx* c, int capacity) {
     if (!c || capacity < 0 || capacity > (1 << 16)) return SR_E_INVALID;
-    if (!hip_ok(hipSetDevice(c->device)) || !hip_ok(hipDeviceSynchronize())) return SR_E_HIP;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     c->tev.assign(4 * (size_t)capacity, nullptr);
     c->timing_cap = 0;

@@ -187,3 +187,38 @@ def test_press_r_sweep_mean_points_pinned(pkg, oracle):
     camera rays returns 468.4 points per ray on average."""
     n = oracle.pressr_sweep(pkg.abi.default_camera(), 1920, 1080, 2000, 2, 0, 1080, 0)
     assert abs(n / (1920 * 1080) - 468.4) < 0.05, n / (1920 * 1080)
+
+
+def test_reference_assets_ingest_layout(pkg):
+    """assets/textures decoded as the app loads them (src/main.cpp:205-218,
+    image_utils.cpp:7-117): vertical flip (row 0 = bottom), RGB skybox, the
+    array padded to 1601x1201 RGBA with alpha 255 inside the RGB layer."""
+    A = pkg.assets
+    if not A.available():
+        pytest.skip("assets/textures missing")
+    from PIL import Image
+
+    bg = A.skybox("2k")
+    assert bg.shape == (1024, 2048, 3) and bg.dtype == np.uint8
+    with Image.open(A.SKYBOX["2k"]) as im:
+        top = np.asarray(im.convert("RGB"))[0]
+    assert np.array_equal(bg[-1], top)  # flipped: the picture's top row is the last row
+    arr, sizes, mx = A.texture_array()
+    assert arr.shape == (2, 1201, 1601, 4) and sizes == [(600, 600), (1601, 1201)] and mx == (1601, 1201)
+    assert (arr[0, :600, :600, 3] == 255).all() and (arr[0, 600:, :, :] == 0).all() and (arr[0, :, 600:] == 0).all()
+    scene = pkg.abi.default_scene()
+    assert [tuple(scene.texture_sizes[i]) for i in range(2)] == [(600.0, 600.0), (1601.0, 1201.0)]
+
+
+def test_flyby_camera_follows_the_hyperbola(pkg):
+    """sr_camera_hyperbolic_trajectory (camera.cpp:20-39): starts on the +z axis
+    at the initial distance, passes the closest distance at t = 0.5, looks at
+    the origin, keeps the fov."""
+    abi = pkg.abi
+    c0, c5, c1 = abi.camera_flyby(0.0), abi.camera_flyby(0.5), abi.camera_flyby(1.0)
+    p0, p5, p1 = (np.array(c.transform.pos[:3], dtype=np.float64) for c in (c0, c5, c1))
+    assert abs(np.linalg.norm(p0) - 30.0) < 1e-3 and p0[2] > 29.99
+    assert abs(np.linalg.norm(p5) - 10.0) < 1e-3 and abs(p1[2] + 30.0) < 1e-3
+    for c, p in ((c0, p0), (c5, p5), (c1, p1)):
+        fwd = np.array(c.transform.axes[6:9], dtype=np.float64)
+        assert np.allclose(fwd, -p / np.linalg.norm(p), atol=1e-5) and c.fov == 90.0

@@ -1,0 +1,64 @@
+"""The multi-rank bench path on the GPU box: bench.py under torchrun with two
+ranks sharing the one leased GPU (gloo backend, tiles staged through host
+memory), three frames in flight, a flyby camera (every frame different).
+Every gathered frame must equal, byte for byte, the frame the single-rank
+run of the same command renders. This executes the distributed init, the
+block-cyclic sr_render_blocks shares, FrameGather, the in-flight pipeline and
+the max-over-ranks timing of bench.py (the 8-GPU run uses the same code with
+the nccl backend). Both runs are child processes: this test process never
+touches the GPU."""
+import json
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+ARGS = ["--width", "320", "--height", "180", "--max-steps", "800", "--steps", "6", "--warmup", "2",
+        "--inflight", "3", "--camera", "flyby", "--cpu-baseline", "off", "--critical-path", "off",
+        "--reference-loop", "off"]
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run(cmd, out):
+    r = subprocess.run(cmd + ARGS + ["--dump-frames", str(out)], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    return json.loads(line)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world):
+    try:
+        import torch
+    except ImportError:
+        pytest.skip("torch missing")
+    single = run([sys.executable, "bench.py", "--gpus", "1"], tmp_path / "one")
+    multi = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                 "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(world),
+                 "--dist-backend", "gloo"], tmp_path / "multi")
+    assert multi["n_gpus"] == world and single["n_gpus"] == 1
+    assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["frames_in_flight"] == 3
+    one = sorted((tmp_path / "one").glob("frame_*.npy"))
+    many = sorted((tmp_path / "multi").glob("frame_*.npy"))
+    assert len(one) == len(many) == 6
+    distinct = set()
+    for a, b in zip(one, many):
+        assert a.name == b.name
+        fa, fb = np.load(a), np.load(b)
+        assert fa.shape == fb.shape == (180, 320, 4)
+        assert np.array_equal(fa, fb), a.name
+        distinct.add(fa.tobytes())
+    assert len(distinct) == 6  # the flyby moves the camera every frame

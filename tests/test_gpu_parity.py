@@ -400,3 +400,31 @@ def test_reseed_headline_rows(pkg, gpu, oracle, oracle_tex, name, pos, fov, u_f)
         rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
         assert (rb[0] != b[y]).any(-1).mean() <= 1e-3, f"{name}: row {y}"
         assert (rs[0] != s[y]).sum() == 0, f"{name}: row {y} step counts"
+
+
+def test_reference_assets_frame(pkg, oracle):
+    """The reference's own textures through the ingest path (assets/textures:
+    2k.jpg skybox, uv_checker.jpg + cubemap.png array, image_utils.cpp:7-117)
+    into sr_set_background / sr_set_texture_array: a 480x270 / 1000-step
+    frame and a flyby view, GPU == oracle on the same decoded texels."""
+    import torch
+
+    A, sc, abi = pkg.assets, pkg.scenes, pkg.abi
+    if not A.available():
+        pytest.skip("assets/textures missing")
+    bg = A.skybox("2k")
+    arr, sizes, mx = A.texture_array()
+    scene = sc.scene_default(textured=True)
+    assert [tuple(scene.texture_sizes[i]) for i in range(2)] == [tuple(float(v) for v in s) for s in sizes]
+    r = pkg.Renderer(0)
+    r.set_background(bg)
+    r.set_texture_array(arr)
+    r.set_scene(scene)
+    tex = oracle.TextureSet(bg, arr)
+    for label, cam in (("default camera", abi.default_camera()), ("flyby t = 0.4", abi.camera_flyby(0.4))):
+        params = abi.default_params(max_steps=1000, percent_black=-1.0)
+        f, b, s = r.render_debug(cam, params, 480, 270)
+        torch.cuda.synchronize()
+        o = oracle.render(scene, cam, params, 480, 270, tex)
+        print(compare((b.cpu().numpy(), f.cpu().numpy(), s.cpu().numpy()), o, label))
+    r.close()

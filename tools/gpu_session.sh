@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
 if [[ $STEPS == *pytest* ]]; then
-  run pytest_gpu 900 python -m pytest tests -m gpu -x -q -rA ${PYTEST_ARGS:-}; rc=$?
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}; rc=$?
   if fatal $rc; then echo "pytest fatal rc=$rc, stopping"; exit $rc; fi
 fi
 if [[ $STEPS == *smoke* ]]; then
@@ -30,5 +30,8 @@ fi
 if [[ $STEPS == *prof* ]]; then
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --cpu-baseline off --critical-path off || exit $?
   find "$OUT/prof" -name "*stats*" -o -name "*kernel_stats*" | head -20
+fi
+if [[ $STEPS == *counters* ]]; then
+  run counters 120 rocprofv3 -L || exit $?
 fi
 echo "session done"
