@@ -73,8 +73,9 @@ def frames_in_flight(width, height, world):
 
 def hw_queues_needed(frames, world, backend):
     """Hardware queues a rank wants: one per in-flight frame's stream, plus
-    the collective's internal streams (RCCL) and the default stream."""
-    return frames + (2 if world > 1 and backend == "nccl" else 0) + 1
+    the collective's internal streams (RCCL) and the default stream; at
+    least 8 (the setting every round-1 measurement ran with)."""
+    return max(8, frames + (2 if world > 1 and backend == "nccl" else 0) + 1)
 
 
 def kernel_sha() -> str:

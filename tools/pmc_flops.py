@@ -100,15 +100,26 @@ def main():
         t = r.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0)
         print(f"{r['kernel']:28s} expect flop {r['flop']:.4g} trans {r['trans']:.4g} | FLOPS_FP32 {f:.4g} "
               f"TRANS {t:.4g} VALU {r.get('SQ_INSTS_VALU', 0):.4g} FMA {r.get('SQ_INSTS_VALU_FMA_F32', 0):.4g}")
-    fma = [r for r in cal if r["flop"] and r.get("SQ_INSTS_VALU_FLOPS_FP32")]
-    k_flop = sum(r["flop"] for r in fma) / sum(r["SQ_INSTS_VALU_FLOPS_FP32"] for r in fma)
-    spread = max(abs(r["flop"] / r["SQ_INSTS_VALU_FLOPS_FP32"] / k_flop - 1.0) for r in fma)
+    # The counter tallies each wave-instruction's FP32 FLOP (FMA 2, packed FMA
+    # 4, add / mul / transcendental 1) once per wave, whatever the exec mask:
+    # the half-active kernel reads the same as the full one. So it measures
+    # the VALU's FP32 issue, 64 lanes per wave-instruction; the factor is
+    # fitted on the full-wave kernels (the epilogue's few adds per wave
+    # keep it a little under 64).
+    full = [r for r in cal if r["flop"] and not r["kernel"].endswith("true>") and r.get("SQ_INSTS_VALU_FLOPS_FP32")]
+    k_flop = sum(r["flop"] for r in full) / sum(r["SQ_INSTS_VALU_FLOPS_FP32"] for r in full)
+    spread = max(abs(r["flop"] / r["SQ_INSTS_VALU_FLOPS_FP32"] / k_flop - 1.0) for r in full)
+    half = [r for r in cal if r["kernel"].endswith("true>")]
+    mask_blind = bool(half) and all(abs(h.get("SQ_INSTS_VALU_FLOPS_FP32", 0) / max(1.0, f.get("SQ_INSTS_VALU_FLOPS_FP32", 1))
+                                        - 1.0) < 0.02 for h in half for f in full[:1])
     tr = [r for r in cal if r["trans"] and r.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS")]
     k_trans = (sum(r["trans"] for r in tr) / sum(r["SQ_INSTS_VALU_FLOPS_FP32_TRANS"] for r in tr)) if tr else k_flop
-    print(f"FLOP per FLOPS_FP32 unit {k_flop:.4g} (max deviation over kernels {spread:.3%}); per TRANS unit {k_trans:.4g}")
+    trans_in_fp32 = bool(tr) and all(r.get("SQ_INSTS_VALU_FLOPS_FP32", 0) >= r["SQ_INSTS_VALU_FLOPS_FP32_TRANS"] for r in tr)
+    print(f"FLOP per FLOPS_FP32 unit {k_flop:.4g} (max deviation over full-wave kernels {spread:.3%}); "
+          f"exec-mask blind: {mask_blind}; transcendentals inside FLOPS_FP32: {trans_in_fp32}; per TRANS unit {k_trans:.4g}")
 
     grid, c, n = frame_counters(args.frame)
-    flop = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * k_flop
+    flop = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * k_flop  # transcendentals included (1 each)
     trans = c.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0) * k_trans
     rec = {
         "kernel": "sr_integrate_kernel<true>",
@@ -118,15 +129,17 @@ def main():
         "max_steps": args.max_steps,
         "grid_threads": grid,
         "dispatches_averaged": max(n.values()) if n else 0,
-        "flop_per_launch": flop + trans,
-        "fp32_flop_per_launch": flop,
+        "flop_per_launch": flop,
         "trans_ops_per_launch": trans,
         "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
-        "calibration": {"flop_per_unit": k_flop, "trans_per_unit": k_trans, "max_deviation": spread},
+        "calibration": {"flop_per_unit": k_flop, "trans_per_unit": k_trans, "max_deviation": spread,
+                        "exec_mask_blind": mask_blind, "trans_inside_fp32": trans_in_fp32},
         "counters": c,
-        "note": ("flop_per_launch = (SQ_INSTS_VALU_FLOPS_FP32 x flop_per_unit + _TRANS x trans_per_unit) per "
-                 "integrate dispatch of the frame grid; units calibrated on flops_calib.hip (v_fma_f32, "
-                 "v_pk_fma_f32, v_add_f32, v_mul_f32 with full and half-active waves, v_rcp_f32)"),
+        "note": ("flop_per_launch = SQ_INSTS_VALU_FLOPS_FP32 x flop_per_unit per integrate dispatch of the frame "
+                 "grid: FP32 FLOP issued by the VALU, 64 lanes per wave-instruction (the counter ignores the exec "
+                 "mask, so lanes of a wave whose rays have ended still count: issue, not useful work); "
+                 "transcendentals count 1. Calibrated on flops_calib.hip (v_fma_f32, v_pk_fma_f32, v_add_f32, "
+                 "v_mul_f32, v_rcp_f32; full and half-active waves)"),
         "source": args.source,
     }
     Path(args.out).write_text(json.dumps(rec, indent=1) + "\n")
