@@ -65,17 +65,31 @@ MODES = {"curved": 0, "flat": 1, "half_width": 2, "half_height": 3}
 FLYBY = (30.0, 10.0)  # src/main.cpp:409: hyperbolicTrajectory(30, 10, t)
 
 
-def frames_in_flight(width, height, world):
-    """Default frames in flight per GPU: 4 while a rank holds at least a
-    quarter of a 1080p frame, 6 below that."""
-    return 4 if width * height / world >= 1920 * 1080 / 4 else 6
+HEADLINE_PX = 1920 * 1080
+MAX_BATCH = 16  # SR_MAX_BATCH (sr_render_blocks_batch)
 
 
-def hw_queues_needed(frames, world, backend):
-    """Hardware queues a rank wants: one per in-flight frame's stream, plus
+def frames_per_launch(width, height, world):
+    """Default frames per launch (sr_render_blocks_batch): a rank's share of B
+    frames, B chosen so that one launch carries about four headline frames'
+    worth of pixels, 1..16. A rank holding 1/N of a frame then runs launches
+    as large as a whole frame's: its share alone is latency-bound (the photon
+    ring's waves) and small concurrent launches fill the GPU badly
+    (profiles/r02/s3_batch_*.jsonl)."""
+    return max(1, min(MAX_BATCH, round(4 * HEADLINE_PX * world / (width * height))))
+
+
+def launches_in_flight(batch):
+    """Default launches in flight per GPU (each on its own context and stream):
+    3 for batched launches, 4 for single frames."""
+    return 3 if batch > 1 else 4
+
+
+def hw_queues_needed(launches, world, backend):
+    """Hardware queues a rank wants: one per in-flight launch's stream, plus
     the collective's internal streams (RCCL) and the default stream; at
     least 8 (the setting every round-1 measurement ran with)."""
-    return max(8, frames + (2 if world > 1 and backend == "nccl" else 0) + 1)
+    return max(8, launches + (2 if world > 1 and backend == "nccl" else 0) + 1)
 
 
 def kernel_sha() -> str:
@@ -107,8 +121,13 @@ def parse():
                     help="BACKGROUND_TEXTURE_QUALITY (src/main.cpp:57-63); auto: 8k for the 8k still, else 2k")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU, each on its own context and stream (0: 4, or 6 when the rank "
-                         "holds under a quarter of a 1080p frame)")
+                    help="launches in flight per GPU, each on its own context and stream (0: 3 for batched "
+                         "launches, 4 for single frames)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per launch, 1..16 (sr_render_blocks_batch; 0: about four headline frames' worth "
+                         "of pixels of this rank's share per launch)")
+    ap.add_argument("--split", default="0",
+                    help="split tiles MAX_TILES[:LANES[:MIN_STEPS]] (sr_set_split; 0: off)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl: RCCL gather of device tiles over xGMI (one GPU per rank); gloo: tiles staged "
                          "through host memory (ranks may share a GPU)")
@@ -135,7 +154,11 @@ def main():
     distributed = world > 1
     W0, H0, N0 = WORKLOADS[args.workload]
     W, H, N = args.width or W0, args.height or H0, args.max_steps or N0
-    F = args.inflight if args.inflight > 0 else frames_in_flight(W, H, world)
+    B = args.batch if args.batch > 0 else frames_per_launch(W, H, world)
+    if not 1 <= B <= MAX_BATCH:
+        raise SystemExit(f"bench: --batch must be 1..{MAX_BATCH}")
+    F = args.inflight if args.inflight > 0 else launches_in_flight(B)
+    split = [int(x) for x in args.split.split(":")] + [16, 1][len(args.split.split(":")) - 1:]
     # every in-flight frame's stream needs a hardware queue of its own (HIP's
     # default is 4 per process); must be set before the HIP runtime starts.
     # Under a profiler whose preloaded library has already started HIP the
@@ -178,17 +201,20 @@ def main():
         skybox = sc.skybox(*((8192, 4096) if quality == "8k" else (2048, 1024)))
         arr, _, _ = sc.default_texture_array()
     # Cameras: frame f of the run (warmup + timed) uses cams[f].
-    n_frames = max(args.warmup, F) + args.steps
+    warm = max(args.warmup, F * B)  # every context learns its launch order
+    n_frames = warm + args.steps
     if args.camera == "flyby":
         cams = [abi.camera_flyby((f + 0.5) / n_frames, *FLYBY) for f in range(n_frames)]
     else:
         cams = [abi.default_camera()] * n_frames
-    # Frames in flight: a frame's time is bounded by the latency of its
-    # longest rays' waves, which a share of 1/N of the rows
-    # does not shorten; independent frames on their own contexts and streams
-    # fill the SIMDs those waves leave idle. Frame f renders on context f % F
-    # and is gathered to rank 0 on that context's stream (nccl), or through
-    # host memory once it is done (gloo).
+    # Launches in flight, B frames per launch: a frame's time is bounded by
+    # the latency of its longest rays' waves, which a share of
+    # 1/N of the rows does not shorten. One launch renders this rank's rows
+    # of B consecutive frames (sr_render_blocks_batch, a camera per frame),
+    # and F launches on their own contexts and streams fill the SIMDs those
+    # waves leave idle. Launch j renders on context j % F; its tiles are
+    # gathered to rank 0 on that context's stream (nccl, one collective per
+    # launch), or through host memory once it is done (gloo).
     D = pkg.dist
     gloo = distributed and args.dist_backend == "gloo"
     ctxs = []
@@ -198,7 +224,8 @@ def main():
         rk.set_background(skybox)
         rk.set_texture_array(arr)
         rk.set_culling(not args.no_cull)
-        tile_k = torch.zeros((D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
+        rk.set_split(split[0], split[1], split[2])
+        tile_k = torch.zeros((B, D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
         host_k = torch.zeros(tuple(tile_k.shape), dtype=torch.uint8).pin_memory() if gloo else None
         gather_k = D.FrameGather(host_k if gloo else tile_k, world, rank, H, BLOCK_ROWS)
         ctxs.append((rk, tile_k, gather_k, torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev),
@@ -208,32 +235,44 @@ def main():
     frames = {}  # --dump-frames: frame index -> assembled frame (rank 0), timed frames only
     dump_from = [1 << 30]
 
-    def keep(f, frame):
-        if args.dump_frames and frame is not None and f >= dump_from[0]:
-            frames[f] = frame.clone()  # on the frame's stream (nccl) or host (gloo)
+    def keep(first, batch):
+        if args.dump_frames and batch is not None:
+            for i in range(batch.shape[0]):
+                if first + i >= dump_from[0]:
+                    frames[first + i] = batch[i].clone()  # on the launch's stream (nccl) or host (gloo)
 
-    def launch(f):
-        rk, tile_k, gather_k, s_k, host_k = ctxs[f % F]
+    def render(rk, first, n, out, s_k):
+        """frames first .. first + n - 1 of this rank's share into out[:n]"""
+        if n == 1:
+            rk.render_blocks(cams[first], params, W, H, BLOCK_ROWS, rank, world, out=out[0], stream=s_k)
+        else:
+            rk.render_blocks_batch(cams[first:first + n], params, W, H, BLOCK_ROWS, rank, world, out=out[:n],
+                                   stream=s_k)
+
+    def launch(j, first, n):
+        rk, tile_k, gather_k, s_k, host_k = ctxs[j % F]
         with torch.cuda.stream(s_k):
-            rk.render_blocks(cams[f], params, W, H, BLOCK_ROWS, rank, world, out=tile_k, stream=s_k)
+            render(rk, first, n, tile_k, s_k)
             if gloo:
-                host_k.copy_(tile_k, non_blocking=True)
+                host_k[:n].copy_(tile_k[:n], non_blocking=True)
                 return
-            keep(f, gather_k())  # the assembled frame on rank 0 (RCCL gather for N > 1)
+            keep(first, gather_k(n))  # the assembled frames on rank 0 (RCCL gather for N > 1)
 
-    def complete(f):  # gloo: the frame's host tile is gathered once its render is done
+    def complete(j, first, n):  # gloo: the launch's host tiles are gathered once its render is done
         if gloo:
-            _, _, gather_k, s_k, _ = ctxs[f % F]
+            _, _, gather_k, s_k, _ = ctxs[j % F]
             s_k.synchronize()
-            keep(f, gather_k())
+            keep(first, gather_k(n))
 
     def run_frames(first, count):
-        for f in range(first, first + count):
-            launch(f)
-            if f - first >= F - 1:
-                complete(f - F + 1)
-        for f in range(max(first, first + count - F + 1), first + count):
-            complete(f)
+        """frames first .. first + count - 1 in launches of B (the last takes the rest), F in flight"""
+        work = [(j, f, min(B, first + count - f)) for j, f in enumerate(range(first, first + count, B))]
+        for i, w in enumerate(work):
+            launch(*w)
+            if i >= F - 1:
+                complete(*work[i - F + 1])
+        for w in work[max(0, len(work) - F + 1):]:
+            complete(*w)
 
     def sync_all():
         for c in ctxs:
@@ -251,13 +290,12 @@ def main():
     band_rows = [int(b) * 16 for b in band_max.argsort(descending=True)[:CRITICAL_CANDIDATES].tolist()] or [0]
     del steps_full, band_max
 
-    warm = max(args.warmup, F)  # every context learns its launch order
     run_frames(0, warm)
     sync_all()
 
-    # ---- the timed region: K frames, F in flight, per-kernel HIP events on
-    # every context's stream (integrate / shade / resume of each frame)
-    per_ctx = -(-args.steps // F) + 1
+    # ---- the timed region: K frames in launches of B, F in flight, per-kernel
+    # HIP events on every context's stream (integrate / shade / resume of each launch)
+    per_ctx = -(-args.steps // (B * F)) + 1
     dump_from[0] = warm
     for c in ctxs:
         c[0].set_timing(per_ctx)
@@ -282,15 +320,16 @@ def main():
         c[0].set_timing(0)
     integrate_ms, shade_ms, resume_ms = (float(x) for x in ktimes.mean(axis=0))
 
-    # single-frame latency (untimed for `value`): one frame alone on context 0
-    lat_frames = 5
+    # frame latency (untimed for `value`): one launch of B frames alone on
+    # context 0; every frame of it is done when the launch is
+    lat_launches = 5
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
-    for f in range(lat_frames):
-        r.render_blocks(cams[warm + f % args.steps], params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+    for _ in range(lat_launches):
+        render(r, warm, min(B, args.steps), tile, stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    latency_ms = ev0.elapsed_time(ev1) / lat_frames
+    latency_ms = ev0.elapsed_time(ev1) / lat_launches
 
     # the reference's loop: one un-culled frame against one culled frame, alone
     speedup_ref = None
@@ -299,7 +338,7 @@ def main():
             r.set_culling(cull)
             r.set_timing(2)
             for _ in range(2):
-                r.render_blocks(cams[0], params, W, H, BLOCK_ROWS, rank, world, out=tile, stream=stream)
+                r.render_blocks(cams[0], params, W, H, BLOCK_ROWS, rank, world, out=tile[0], stream=stream)
             torch.cuda.synchronize(dev)
             t = float(r.kernel_times(2)[-1, 0])
             r.set_timing(0)
@@ -353,7 +392,7 @@ def main():
                     "frac_of_frame_latency": round(band_ms / latency_ms, 3)}
 
     if rank == 0:
-        roofline = make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, resume_ms,
+        roofline = make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_ms, resume_ms,
                                  latency_ms, sigma_steps_frame, sigma_steps_mine, len(rows_mine), critical,
                                  speedup_ref)
         cpu = None
@@ -390,7 +429,10 @@ def main():
                 "tiling": (f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), "
                            + ("RCCL gather to rank 0" if not gloo else "gloo gather of host-staged tiles to rank 0")),
                 "dist_backend": args.dist_backend if distributed else None,
-                "frames_in_flight": F,
+                "launches_in_flight": F,
+                "frames_per_launch": B,
+                "frames_in_flight": F * B,
+                "split_tiles": args.split,
                 "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "frame_latency_ms": round(latency_ms, 4),
                 "culling": not args.no_cull,
@@ -422,7 +464,7 @@ def load_matching(path, W, H, N, world):
     return rec
 
 
-def make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, resume_ms, latency_ms,
+def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_ms, resume_ms, latency_ms,
                   sigma_steps_frame, sigma_steps_mine, rows_mine, critical, speedup_ref):
     """Roofline of the dominant kernel (sr_integrate_kernel: ray generation,
     the step loop and every intersection test), on rank 0's launches.
@@ -434,9 +476,10 @@ def make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, 
     tools/microbench/flops_calib.hip: profiles/pmc_latest.json) times the
     launches per second of this run (one per frame, F in flight), so `frac`
     is utilisation of the FP32 peak. `kernel_ms` is the same run's mean
-    integrate-launch duration (HIP events on each frame's stream; launches
-    overlap F-fold, `overlap` = kernel_ms / ms_per_step): it is what the
-    rocprofv3 --stats summary of this command reports."""
+    integrate-launch duration (HIP events on each launch's stream; a launch
+    renders B frames and F launches overlap, `overlap` = kernel_ms / (B x
+    ms_per_step)): it is what the rocprofv3 --stats summary of this command
+    reports."""
     pmc = load_matching(args.pmc_json, W, H, N, world)
     share = sigma_steps_mine / max(1, sigma_steps_frame)  # rank 0's share of the frame's steps
     executed = None
@@ -465,8 +508,9 @@ def make_roofline(args, W, H, N, world, F, ms_per_step, integrate_ms, shade_ms, 
         "executed_flop_per_launch": None if executed is None else round(executed),
         "valu_issue_frac": None if valu_issue is None else round(valu_issue, 4),
         "kernel_ms": round(integrate_ms, 4),
-        "overlap": round(integrate_ms / ms_per_step, 2),
-        "frames_in_flight": F,
+        "overlap": round(integrate_ms / (B * ms_per_step), 2),
+        "launches_in_flight": F,
+        "frames_per_launch": B,
         "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
                         "resume": round(resume_ms, 4)},
         "steps_per_launch": sigma_steps_mine,

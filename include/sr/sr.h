@@ -283,12 +283,32 @@ int sr_render_blocks(sr_ctx* ctx, const sr_camera* cam, const sr_params* params,
                      int height, int block_rows, int block_first, int block_step,
                      uint8_t* dev_rgba8, size_t pitch_bytes, sr_stream stream);
 
+/* Frames in one launch (not in the reference; the pixels are unchanged): the
+ * rows sr_render_blocks would render, for n_frames (1 .. 16) frames that
+ * differ only in the camera (cams[f]), frame f packed at dev_rgba8 + f *
+ * frame_stride_bytes. One launch carries n_frames times the work, so a GPU
+ * holding a small share of each frame (multi-GPU row tiling) runs it as
+ * efficiently as a whole frame; the launch order and split tiles follow the
+ * costliest tiles over the batch. SR_E_CAPACITY above 16 frames. */
+int sr_render_blocks_batch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params,
+                           int width, int height, int block_rows, int block_first, int block_step,
+                           uint8_t* dev_rgba8, size_t pitch_bytes, size_t frame_stride_bytes, sr_stream stream);
+
 /* Debug/parity variant: unclamped FragColor as float RGBA (dev_rgba32, may be
  * NULL), the RGBA8 pixel (dev_rgba8, may be NULL) and the number of executed
  * geodesic steps per pixel (dev_steps, may be NULL). Dense rows. */
 int sr_render_debug(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width,
                     int height, int row_begin, int row_end, float* dev_rgba32,
                     uint8_t* dev_rgba8, int32_t* dev_steps, sr_stream stream);
+
+/* Split tiles (not in the reference; a latency knob, the pixels are unchanged):
+ * the next frames run the max_tiles costliest 16x16 workgroup tiles of the
+ * previous frame on this context whose longest ray took at least min_steps
+ * steps as waves of lanes_per_wave (16, 4 or 1) rays instead of 64. A wave's
+ * budget events are the union of its rays' events, so the frame's longest
+ * rays finish sooner in sparse waves, at the cost of more waves for those
+ * tiles. max_tiles 0 (the default) turns it off. */
+int sr_set_split(sr_ctx* ctx, int max_tiles, int lanes_per_wave, int min_steps);
 
 /* Rows a sr_render_blocks call with these arguments writes. */
 int sr_blocks_row_count(int height, int block_rows, int block_first, int block_step);

@@ -185,6 +185,9 @@ SIGNATURES = {
     "sr_render_blocks": (_i, [_p, C.POINTER(Camera), C.POINTER(Params), _i, _i, _i, _i, _i, _p, C.c_size_t, _p]),
     "sr_render_debug": (_i, [_p, C.POINTER(Camera), C.POINTER(Params), _i, _i, _i, _i, _p, _p, _p, _p]),
     "sr_blocks_row_count": (_i, [_i, _i, _i, _i]),
+    "sr_set_split": (_i, [_p, _i, _i, _i]),
+    "sr_render_blocks_batch": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, _i, _i, _p,
+                                    C.c_size_t, C.c_size_t, _p]),
     "sr_abi_struct_sizes": (_i, [C.POINTER(C.c_size_t), _i]),
     "sr_test_ray_points": (_i, [C.POINTER(C.c_float), C.POINTER(C.c_float), _i, _i, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
 }
@@ -193,6 +196,7 @@ EXTRA_SIGNATURES = {
     "sr_debug_set_culling": (_i, [_p, _i]),
     "sr_debug_set_timing": (_i, [_p, _i]),
     "sr_debug_kernel_times": (_i, [_p, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
+    "sr_debug_last_order": (_i, [_p, C.POINTER(_i), _i, C.POINTER(_i)]),
 }
 
 _lib = None

@@ -128,11 +128,23 @@ typedef struct {
     float max_texture_size[2];
 } sr_dev_scene;
 
+// One frame's camera (Camera::loadShader, camera.cpp:41-50).
+typedef struct {
+    float pos[3];
+    float axes[9];
+    float ray_forward;  // 1 / tan(fov/360*PI), computed once on the host (frag:859)
+} sr_dev_cam;
+
+// Frames one launch renders (sr_render_blocks_batch): the same rows of
+// `batch` frames that differ only in the camera.
+#define SR_MAX_BATCH 16
+
 // Per-launch constants (kernel argument, scalar-loaded).
 typedef struct {
-    float cam_pos[3];
-    float cam_axes[9];
-    float ray_forward;  // 1 / tan(fov/360*PI), computed once on the host (frag:859)
+    sr_dev_cam cam[SR_MAX_BATCH];  // cam[f]: frame f of the batch
+    int32_t batch;      // frames in the launch (1 .. SR_MAX_BATCH)
+    int32_t tiles;      // 16x16 workgroup tiles per frame
+    int64_t out_frame_stride;  // bytes between the frames' output tiles
     float max_angle;    // 2 * max_revolutions * PI (frag:860)
     float res_x, res_y; // resolution uniform == frame size
     float u_f;
@@ -154,6 +166,12 @@ typedef struct {
     // textures (RGBA8 texels)
     int32_t bg_w, bg_h;
     int32_t arr_w, arr_h, arr_layers;
+    // split tiles (sr_set_split): the split_tiles costliest workgroup tiles of
+    // the previous frame (max steps >= split_min_steps) run as 64 >> split_log2
+    // workgroups of 2^split_log2-lane waves; 0 = off
+    int32_t split_tiles;
+    int32_t split_log2;
+    int32_t split_min_steps;
 } sr_dev_frame;
 
 #endif

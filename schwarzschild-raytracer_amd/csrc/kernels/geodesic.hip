@@ -13,6 +13,7 @@
 // transcendentals rounded to binary32, GLSL evaluation order.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <type_traits>
 
 // constant address space: wave-uniform loads through it are scalar loads
@@ -109,6 +110,11 @@ __device__ __forceinline__ void stat_add(int k, unsigned long long v) {
 #endif
 #else
 #define SR_STAT(k, v) ((void)0)
+#endif
+
+#ifdef SR_LANE_MASK
+// Latency experiments only: a per-pixel keep mask (device pointer) over the full frame
+__device__ const uint8_t* sr_lane_mask;
 #endif
 
 #ifdef SR_PROF
@@ -1322,13 +1328,13 @@ __device__ __forceinline__ f4 crosshair_frag(const sr_dev_frame& fr, const Pix& 
 
 // frag:859-889: camera ray, flat / percent_black early outs and the initial
 // (u, du) of the geodesic. Returns ST_FLAT, ST_DONE or -1 (integrate).
-__device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const Pix& q, Ray& r) {
+__device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const sr_dev_cam& cam, const Pix& q, Ray& r) {
     // full_screen_quad.vert:7-10: uv = NDC of the pixel centre
     f2 uv = F2((float)(2 * q.px + 1) / (float)fr.width - 1.0f, (float)(2 * q.py + 1) / (float)fr.height - 1.0f);
     f2 uvv = F2(uv.x, uv.y * fr.res_y / fr.res_x);
-    m3 cam = ldm(fr.cam_axes);
-    r.ro = ld3(fr.cam_pos);
-    r.rd = nrm(mv(cam, F3(uvv.x, uvv.y, fr.ray_forward)));
+    m3 axes = ldm(cam.axes);
+    r.ro = ld3(cam.pos);
+    r.rd = nrm(mv(axes, F3(uvv.x, uvv.y, cam.ray_forward)));
     r.nv = nrm(r.ro);
     r.steps = 0;
     r.i = 0;
@@ -1721,15 +1727,47 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #define SR_MIN_WAVES_PER_EU 6
 #endif
 
-// 1-D grid: launch slot s renders workgroup tile order[s] (costliest first,
-// sr_order_kernel), and records the tile's cost (max steps of its rays).
+// Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
+// tile << 8 | SR_SPLIT | sub for workgroup `sub` of a split tile; -1 for an
+// unused slot of the grid.
+#define SR_SPLIT 0x80
+
+// The thread index (in the tile's own 256-thread numbering, pixel_of) that
+// thread `tid` of split workgroup `sub` stands for, or -1 (idle lane). A split
+// tile's 256 pixels are cut into cells of L = 2^lg pixels (4x4, 2x2 or 1x1
+// squares inside the tile's 8x8 wave tiles); split workgroup `sub` runs cells
+// 4 sub .. 4 sub + 3, one per wave, in lanes 0 .. L - 1. A ray's result does
+// not depend on its wave-mates (every culling decision is exact), so the
+// cells' pixels are bit-identical to the whole tile's.
+__device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
+    const int lane = tid & 63;
+    if (lane >= (1 << lg)) return -1;
+    const int cell = sub * 4 + (tid >> 6);
+    const int side = lg >> 1;                 // cell side 2^side
+    const int cpq = 64 >> lg;                 // cells per 8x8 wave tile
+    const int quad = cell / cpq, qc = cell % cpq;
+    const int per_row = 8 >> side;
+    const int x8 = ((qc % per_row) << side) + (lane & ((1 << side) - 1));
+    const int y8 = ((qc / per_row) << side) + (lane >> side);
+    return quad * 64 + y8 * 8 + x8;
+}
+
+// 1-D grid: workgroup s renders launch code order[s / B] of frame s % B of
+// the batch (costliest tiles of every frame first, sr_order_kernel), and
+// records the tile's cost (max steps of its rays over the batch).
 template <bool CULL>
 __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
     size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
-    const int block = order ? order[blockIdx.x] : (int)blockIdx.x;
+    const unsigned B = (unsigned)fr.batch;
+    const int frame = B > 1 ? (int)(blockIdx.x % B) : 0;
+    const unsigned slot = B > 1 ? blockIdx.x / B : blockIdx.x;
+    const int code = order ? order[slot] : ((int)slot << 8);
     if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+    if (code < 0) return;  // unused slot of a split grid
+    const int block = code >> 8;
+    const int tid = (code & SR_SPLIT) ? split_thread(code & 0x3f, (int)threadIdx.x, fr.split_log2) : (int)threadIdx.x;
 #ifndef SR_PRIO_BLOCKS
 #define SR_PRIO_BLOCKS 256
 #endif
@@ -1737,7 +1775,11 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     // 2000-step ray sharing its SIMD with four other waves would run 3x longer
     // than the rest of the grid. Raised issue priority keeps them near their
     // own latency bound while the other waves fill the idle issue slots.
+#ifdef SR_PRIO_SPLIT
+    if (order && ((code & SR_SPLIT) || blockIdx.x < SR_PRIO_BLOCKS)) __builtin_amdgcn_s_setprio(3);
+#else
     if (order && blockIdx.x < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
+#endif
 #ifdef SR_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     unsigned long long evmat = 0;
@@ -1750,8 +1792,8 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     if ((threadIdx.x & 63) < SR_PROF_N) prof_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     const unsigned long long prof_t0 = clock64();
 #endif
-    if (pixel_of(fr, block, threadIdx.x, q)) {
-        const size_t id = (size_t)block * 256 + threadIdx.x;
+    if (tid >= 0 && pixel_of(fr, block, tid, q)) {
+        const size_t id = ((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256 + tid;
         Tex tx;
         tx.bg = nullptr;
         tx.arr = arr;
@@ -1760,7 +1802,10 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
         const PS& ps = log.ps;
         Ray r;
         Hit hit;
-        int st = init_pixel(fr, q, r);
+        int st = init_pixel(fr, fr.cam[frame], q, r);
+#ifdef SR_LANE_MASK  // latency experiments only (tools/lane_mask.py): masked pixels run no ray
+        if (sr_lane_mask && !sr_lane_mask[(size_t)q.py * fr.width + q.px]) st = ST_DONE;
+#endif
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
@@ -1830,11 +1875,17 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
 // Launch order for the next frame: workgroup tiles by descending cost of this
 // frame (counting sort on 256 cost buckets), so the long rays - those
 // orbiting near the photon sphere run to max_steps - start first instead of
-// forming a latency-bound tail. Resets the costs. One workgroup.
+// forming a latency-bound tail. With split tiles, the first min(split_tiles,
+// tiles of cost >= split_min_steps) tiles are emitted as 64 >> split_log2
+// split workgroups each (their waves carry a few rays: a wave's budget events
+// are the union of its lanes', so the longest rays run with fewer events);
+// the grid's remaining slots get -1. Resets the costs. One workgroup.
 __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, int n, int max_cost,
-                                                        int* __restrict__ order) {
+                                                        int* __restrict__ order, int split_tiles, int split_log2,
+                                                        int split_min) {
     __shared__ int hist[256];
     __shared__ int offs[256];
+    __shared__ int nsplit;
     const int t = threadIdx.x;
     auto bucket = [&](int c) {
         long long b = (long long)(c < 0 ? 0 : c) * 256 / ((long long)max_cost + 1);
@@ -1845,18 +1896,28 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
     for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(cost[i])], 1);
     __syncthreads();
     if (t == 0) {
-        int run = 0;
+        int run = 0, hi = 0;
+        const int bmin = bucket(split_min < 1 ? 1 : split_min);
         for (int b = 255; b >= 0; b--) {
             offs[b] = run;
             run += hist[b];
+            if (b >= bmin) hi += hist[b];
         }
+        nsplit = split_tiles < hi ? split_tiles : hi;
     }
     __syncthreads();
+    const int S = 64 >> split_log2;  // split workgroups per tile
+    const int ns = nsplit;
     for (int i = t; i < n; i += 1024) {
-        const int c = cost[i];
-        order[atomicAdd(&offs[bucket(c)], 1)] = i;
+        const int p = atomicAdd(&offs[bucket(cost[i])], 1);
+        if (p < ns) {
+            for (int sub = 0; sub < S; sub++) order[p * S + sub] = (i << 8) | SR_SPLIT | sub;
+        } else {
+            order[ns * S + (p - ns)] = i << 8;
+        }
         cost[i] = 0;
     }
+    for (int j = n + (S - 1) * ns + t; j < n + (S - 1) * split_tiles; j += 1024) order[j] = -1;
 }
 
 __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __restrict__ sc,
@@ -1867,10 +1928,14 @@ __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __res
                                                       uint8_t* __restrict__ out, size_t pitch,
                                                       float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
                                                       int* __restrict__ list, int* __restrict__ count) {
-    const int block = blockIdx.y * gridDim.x + blockIdx.x;
+    const int vblock = blockIdx.y * gridDim.x + blockIdx.x;  // frame f's tiles are rows f*gy .. of the grid
+    const int f = vblock / fr.tiles, block = vblock - f * fr.tiles;
     Pix q;
     if (!pixel_of(fr, block, threadIdx.x, q)) return;
-    const size_t id = (size_t)block * 256 + threadIdx.x;
+    const size_t id = (size_t)vblock * 256 + threadIdx.x;
+    if (out) out += (size_t)f * (size_t)fr.out_frame_stride;
+    if (dbg_rgba) dbg_rgba += (size_t)f * (size_t)fr.width * (size_t)fr.nrows * 4;
+    if (dbg_steps) dbg_steps += (size_t)f * (size_t)fr.width * (size_t)fr.nrows;
     const PS ps{ps_base, ps_n};
     Tex tx;
     tx.bg = bg;
@@ -1925,8 +1990,9 @@ __global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __re
     tx.opq = nullptr;
     for (int w = blockIdx.x * 256 + threadIdx.x; w < total; w += gridDim.x * 256) {
         const int id = list[w];
+        const int f = (id >> 8) / fr.tiles;
         Pix q;
-        pixel_of(fr, id >> 8, id & 255, q);
+        pixel_of(fr, (id >> 8) - f * fr.tiles, id & 255, q);
         Ray r;
         f4 frag = ps.get4(PS_FRAG, id);
         r.ro = ps.get3(PS_RO, id);
@@ -1951,7 +2017,9 @@ __global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __re
             finish_ray(sc, segs, fr, tx, st, r.ro, r.rd, frag);
             break;
         }
-        write_pixel(fr, out, pitch, dbg_rgba, dbg_steps, q, frag, r.steps);
+        const size_t fo = (size_t)f * (size_t)fr.width * (size_t)fr.nrows;
+        write_pixel(fr, out ? out + (size_t)f * (size_t)fr.out_frame_stride : nullptr, pitch,
+                    dbg_rgba ? dbg_rgba + 4 * fo : nullptr, dbg_steps ? dbg_steps + fo : nullptr, q, frag, r.steps);
     }
 }
 
@@ -1966,21 +2034,29 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     dim3 grid((fr->width + 15) / 16, (fr->nrows + 15) / 16);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
     const unsigned nblocks = grid.x * grid.y;
-    if ((size_t)nblocks * 256 > ps_n) return hipErrorInvalidValue;
+    const unsigned B = (unsigned)fr->batch;
+    if (B < 1 || B > SR_MAX_BATCH || fr->tiles != (int)nblocks) return hipErrorInvalidValue;
+    if ((size_t)nblocks * B * 256 > ps_n || (size_t)nblocks * B * 256 > (size_t)INT32_MAX) return hipErrorInvalidValue;
     if ((order == nullptr) != (cost == nullptr)) return hipErrorInvalidValue;
+    // split tiles need the launch order (their codes come from sr_order_kernel)
+    const int split = order ? fr->split_tiles : 0;
+    if (split < 0 || (split && (fr->split_log2 < 0 || fr->split_log2 > 4 || (fr->split_log2 & 1))))
+        return hipErrorInvalidValue;
+    if (nblocks > (1u << 22)) return hipErrorInvalidValue;  // tile << 8 stays a positive int
+    const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (cull)
-        hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(nblocks), block, 0, stream, sc, tbl, segs, arr, opq, *fr,
-                           ps, ps_n, count, order, cost);
+        hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B), block, 0, stream, sc, tbl, segs, arr, opq,
+                           *fr, ps, ps_n, count, order, cost);
     else
-        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(nblocks), block, 0, stream, sc, tbl, segs, arr, opq, *fr,
-                           ps, ps_n, count, order, cost);
+        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(slots * B), block, 0, stream, sc, tbl, segs, arr, opq,
+                           *fr, ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
-    hipLaunchKernelGGL(sr_shade_kernel, grid, block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n, out, pitch, dbg_rgba,
-                       dbg_steps, list, count);
+    hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
+                       out, pitch, dbg_rgba, dbg_steps, list, count);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
-    unsigned nb = nblocks < 1024u ? nblocks : 1024u;
+    unsigned nb = nblocks * B < 1024u ? nblocks * B : 1024u;
     if (cull)
         hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
@@ -1988,7 +2064,8 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
         hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     if (order)
-        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(1024), 0, stream, cost, (int)nblocks, fr->max_steps, order);
+        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(1024), 0, stream, cost, (int)nblocks, fr->max_steps, order,
+                           split, split ? fr->split_log2 : 6, fr->split_min_steps);
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }
@@ -2001,6 +2078,12 @@ extern "C" int sr_debug_prof(unsigned long long* out, int n_waves) {
         hipSuccess)
         return -3;
     return 0;
+}
+#endif
+
+#ifdef SR_LANE_MASK
+extern "C" int sr_debug_set_lane_mask(const uint8_t* dev_mask) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(sr_lane_mask), &dev_mask, sizeof dev_mask) == hipSuccess ? 0 : -3;
 }
 #endif
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -62,7 +63,11 @@ struct sr_ctx {
         int* order = nullptr;
         int* cost = nullptr;
     };
-    std::map<std::pair<int, int>, Order> orders;
+    std::map<std::array<int, 4>, Order> orders;  // (gx, gy, split_tiles, split_log2)
+    // split tiles (sr_set_split): 0 = off
+    int split_tiles = 0, split_log2 = 4, split_min_steps = 1;
+    const int* last_order = nullptr;  // the launch codes of the context's last frame (its next frame's order)
+    size_t last_slots = 0;
     // the stream of the context's last launch: a context is used from one
     // stream, so waiting for it waits for every frame that
     // may still read the context's buffers, and for nothing else on the device
@@ -413,9 +418,12 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
 
 // Launch order for a grid shape: tiles nearest the frame centre first (where
 // the black hole usually is) until a frame has measured the costs. One
-// buffer pair per shape, allocated on first use.
+// buffer pair per shape and split setting, allocated on first use. Entries
+// are launch codes (geodesic.hip sr_order_kernel): tile << 8 for a whole
+// tile, -1 for the split grid's slots no tile uses yet.
 int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
-    auto key = std::make_pair(gx, gy);
+    const int split = ctx->split_tiles;
+    const std::array<int, 4> key{gx, gy, split, split ? ctx->split_log2 : 0};
     auto it = ctx->orders.find(key);
     if (it != ctx->orders.end()) {
         *order = it->second.order;
@@ -423,6 +431,7 @@ int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
         return SR_OK;
     }
     const size_t n = (size_t)gx * gy;
+    const size_t slots = n + (size_t)((64 >> (split ? ctx->split_log2 : 6)) - 1) * (size_t)split;
     std::vector<int> ord(n);
     std::vector<double> d(n);
     for (size_t i = 0; i < n; i++) {
@@ -431,12 +440,14 @@ int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
         d[i] = x * x + y * y;
     }
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return d[a] < d[b]; });
+    for (int& v : ord) v <<= 8;
+    ord.resize(slots, -1);
     sr_ctx::Order o;
-    if (!hip_ok(hipMalloc(&o.order, n * sizeof(int))) || !hip_ok(hipMalloc(&o.cost, n * sizeof(int)))) {
+    if (!hip_ok(hipMalloc(&o.order, slots * sizeof(int))) || !hip_ok(hipMalloc(&o.cost, n * sizeof(int)))) {
         if (o.order) (void)hipFree(o.order);
         return SR_E_NOMEM;
     }
-    if (!hip_ok(hipMemcpy(o.order, ord.data(), n * sizeof(int), hipMemcpyHostToDevice)) ||
+    if (!hip_ok(hipMemcpy(o.order, ord.data(), slots * sizeof(int), hipMemcpyHostToDevice)) ||
         !hip_ok(hipMemset(o.cost, 0, n * sizeof(int)))) {
         (void)hipFree(o.order);
         (void)hipFree(o.cost);
@@ -448,16 +459,22 @@ int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
     return SR_OK;
 }
 
+// Camera::loadShader (camera.cpp:41-50) and frag:859's launch invariant
+void build_cam(const sr_camera* cam, sr_dev_cam& dc) {
+    std::memcpy(dc.pos, cam->transform.pos, sizeof dc.pos);
+    std::memcpy(dc.axes, cam->transform.axes, sizeof dc.axes);
+    dc.ray_forward = 1.0f / (float)std::tan((double)(cam->fov / 360.0f * kPi));
+}
+
 int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
     if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
     if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
     if (p->filter_mode != SR_FILTER_LERP && p->filter_mode != SR_FILTER_WEIGHTED) return SR_E_INVALID;
     if (p->max_steps < 0 || p->max_steps > (1 << 24)) return SR_E_INVALID;
     std::memset(&fr, 0, sizeof fr);
-    std::memcpy(fr.cam_pos, cam->transform.pos, sizeof fr.cam_pos);
-    std::memcpy(fr.cam_axes, cam->transform.axes, sizeof fr.cam_axes);
-    // frag:859-860 (launch invariants, same float ops)
-    fr.ray_forward = 1.0f / (float)std::tan((double)(cam->fov / 360.0f * kPi));
+    build_cam(cam, fr.cam[0]);
+    fr.batch = 1;
+    // frag:860 (launch invariant, same float ops)
     fr.max_angle = 2.0f * (float)p->max_revolutions * kPi;
     fr.res_x = (float)width;
     fr.res_y = (float)height;
@@ -477,19 +494,31 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.arr_w = ctx->arr_w;
     fr.arr_h = ctx->arr_h;
     fr.arr_layers = ctx->arr_layers;
+    fr.split_tiles = ctx->split_tiles;
+    fr.split_log2 = ctx->split_log2;
+    fr.split_min_steps = ctx->split_min_steps;
     return SR_OK;
 }
 
-int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width, int height, int nrows,
-           int row_base, int block_rows, int block_stride, uint8_t* out, size_t pitch, float* dbg_rgba,
-           int32_t* dbg_steps, sr_stream stream) {
+// Renders the same rows of n_frames frames (cams[f]; output f at out + f *
+// frame_stride) in one launch of each kernel.
+int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params, int width, int height,
+           int nrows, int row_base, int block_rows, int block_stride, uint8_t* out, size_t pitch,
+           size_t frame_stride, float* dbg_rgba, int32_t* dbg_steps, sr_stream stream) {
     if (!ctx) return SR_E_INVALID;
     if (!ctx->scene_set) return SR_E_NOT_READY;
+    if (!cams || n_frames < 1) return SR_E_INVALID;
+    if (n_frames > SR_MAX_BATCH) return SR_E_CAPACITY;
     sr_dev_frame fr;
-    int rc = build_frame(ctx, cam, params, width, height, fr);
+    int rc = build_frame(ctx, cams, params, width, height, fr);
     if (rc != SR_OK) return rc;
+    for (int f = 1; f < n_frames; f++) build_cam(&cams[f], fr.cam[f]);
+    fr.batch = n_frames;
     if (nrows < 0 || block_rows <= 0) return SR_E_INVALID;
     if (out && pitch < (size_t)width * 4) return SR_E_INVALID;
+    if (n_frames > 1 && (!out || frame_stride < pitch * (size_t)nrows || dbg_rgba || dbg_steps)) return SR_E_INVALID;
+    fr.out_frame_stride = (int64_t)frame_stride;
+    fr.tiles = ((width + 15) / 16) * ((nrows + 15) / 16);
     fr.nrows = nrows;
     fr.row_base = row_base;
     fr.block_rows = block_rows;
@@ -498,13 +527,16 @@ int launch(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
     if (rc != SR_OK) return rc;
-    rc = ensure_pixel_state(ctx, (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) * 256);
+    rc = ensure_pixel_state(ctx, (size_t)fr.tiles * (size_t)n_frames * 256);
     if (rc != SR_OK) return rc;
     int* order = nullptr;
     int* cost = nullptr;
     if (nrows > 0) {
         rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, &order, &cost);
         if (rc != SR_OK) return rc;
+        ctx->last_order = order;
+        ctx->last_slots = (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) +
+                          (size_t)((64 >> (ctx->split_tiles ? ctx->split_log2 : 6)) - 1) * (size_t)ctx->split_tiles;
     }
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
@@ -738,7 +770,7 @@ int sr_render(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, in
               int row_end, uint8_t* out, size_t pitch, sr_stream stream) {
     if (!out || row_begin < 0 || row_end > height || row_begin > row_end) return SR_E_INVALID;
     int n = row_end - row_begin;
-    return launch(c, cam, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, pitch, nullptr, nullptr,
+    return launch(c, cam, 1, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, pitch, 0, nullptr, nullptr,
                   stream);
 }
 
@@ -757,8 +789,18 @@ int sr_render_blocks(sr_ctx* c, const sr_camera* cam, const sr_params* p, int wi
     if (!out || block_rows <= 0 || block_first < 0 || block_step <= 0) return SR_E_INVALID;
     int nblocks = 0;
     for (int b = block_first; b * block_rows < height; b += block_step) nblocks++;
-    return launch(c, cam, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
-                  block_step * block_rows, out, pitch, nullptr, nullptr, stream);
+    return launch(c, cam, 1, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
+                  block_step * block_rows, out, pitch, 0, nullptr, nullptr, stream);
+}
+
+int sr_render_blocks_batch(sr_ctx* c, const sr_camera* cams, int n_frames, const sr_params* p, int width,
+                           int height, int block_rows, int block_first, int block_step, uint8_t* out, size_t pitch,
+                           size_t frame_stride, sr_stream stream) {
+    if (!out || block_rows <= 0 || block_first < 0 || block_step <= 0) return SR_E_INVALID;
+    int nblocks = 0;
+    for (int b = block_first; b * block_rows < height; b += block_step) nblocks++;
+    return launch(c, cams, n_frames, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
+                  block_step * block_rows, out, pitch, frame_stride, nullptr, nullptr, stream);
 }
 
 int sr_render_debug(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, int height, int row_begin,
@@ -766,7 +808,7 @@ int sr_render_debug(sr_ctx* c, const sr_camera* cam, const sr_params* p, int wid
     if (row_begin < 0 || row_end > height || row_begin > row_end) return SR_E_INVALID;
     if (!dbg_rgba && !out && !dbg_steps) return SR_E_INVALID;
     int n = row_end - row_begin;
-    return launch(c, cam, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, (size_t)width * 4, dbg_rgba,
+    return launch(c, cam, 1, p, width, height, n, row_begin, n > 0 ? n : 1, 0, out, (size_t)width * 4, 0, dbg_rgba,
                   dbg_steps, stream);
 }
 
@@ -775,6 +817,34 @@ int sr_abi_struct_sizes(size_t* out, int n) {
                           sizeof(sr_test_ray), sizeof(sr_material), sizeof(sr_light)};
     if (!out || n < 0) return SR_E_INVALID;
     for (int i = 0; i < n && i < 6; i++) out[i] = sz[i];
+    return SR_OK;
+}
+
+int sr_set_split(sr_ctx* c, int max_tiles, int lanes_per_wave, int min_steps) {
+    if (!c || max_tiles < 0 || max_tiles > (1 << 16) || min_steps < 0) return SR_E_INVALID;
+    int lg;
+    switch (lanes_per_wave) {
+    case 16: lg = 4; break;
+    case 4: lg = 2; break;
+    case 1: lg = 0; break;
+    default: return SR_E_INVALID;
+    }
+    c->split_tiles = max_tiles;
+    c->split_log2 = lg;
+    c->split_min_steps = min_steps;
+    return SR_OK;
+}
+
+// Not in sr.h's public set: the launch codes sr_order_kernel wrote at the end
+// of the context's last frame (the next frame of that shape runs them; tile
+// << 8, | 0x80 | sub for split workgroups, -1 unused). Waits for the frame.
+int sr_debug_last_order(sr_ctx* c, int* out, int max_n, int* n) {
+    if (!c || !n || max_n < 0 || (max_n && !out)) return SR_E_INVALID;
+    *n = (int)c->last_slots;
+    if (!c->last_order) return SR_OK;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
+    const size_t k = c->last_slots < (size_t)max_n ? c->last_slots : (size_t)max_n;
+    if (k && !hip_ok(hipMemcpy(out, c->last_order, k * sizeof(int), hipMemcpyDeviceToHost))) return SR_E_HIP;
     return SR_OK;
 }
 

@@ -42,7 +42,16 @@ def tile_rows(world: int, height: int, block_rows: int) -> int:
 
 def assemble(stacked, world: int, height: int, block_rows: int):
     """[world, tile_rows, W, C] gathered tiles (rank order) -> [height, W, C]
-    frame. numpy arrays or torch tensors."""
+    frame. numpy arrays or torch tensors. Batched tiles [world, B, tile_rows,
+    W, C] -> [B, height, W, C] frames."""
+    if stacked.ndim == 5:
+        B = stacked.shape[1]
+        if isinstance(stacked, np.ndarray):
+            return np.stack([assemble(stacked[:, b], world, height, block_rows) for b in range(B)])
+        tr, rest = stacked.shape[2], tuple(stacked.shape[3:])
+        per = tr // block_rows
+        v = stacked.reshape((world, B, per, block_rows) + rest).permute((1, 2, 0, 3) + tuple(range(4, 4 + len(rest))))
+        return v.reshape((B, per * world * block_rows) + rest)[:, :height]
     w, tr = stacked.shape[0], stacked.shape[1]
     assert w == world and tr % block_rows == 0
     rest = tuple(stacked.shape[2:])
@@ -56,7 +65,9 @@ def assemble(stacked, world: int, height: int, block_rows: int):
 
 
 class FrameGather:
-    """Preallocated gather of equal-size tiles to rank 0 (collective)."""
+    """Preallocated gather of equal-size tiles to rank 0 (collective). A tile
+    of [B, tile_rows, W, C] holds B frames (a batched launch); __call__(n)
+    gathers the first n of them and returns the [n, H, W, C] frames."""
 
     def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None):
         self.world, self.rank, self.height, self.block_rows, self.group = world, rank, height, block_rows, group
@@ -67,14 +78,18 @@ class FrameGather:
             self.stacked = tile.new_empty((world,) + tuple(tile.shape))
             self.views = [self.stacked[i] for i in range(world)]
 
-    def __call__(self, assemble_frame: bool = True):
+    def __call__(self, n: int | None = None, assemble_frame: bool = True):
         import torch.distributed as dist
 
+        tile, views, stacked = self.tile, self.views, self.stacked
+        if n is not None:  # batched tile: its first n frames
+            tile = tile[:n]
+            views = None if views is None else [v[:n] for v in views]
+            stacked = None if stacked is None else stacked[:, :n]
         if self.world == 1:
-            stacked = self.tile[None]
+            stacked = tile[None]
         else:
-            dist.gather(self.tile, self.views if self.rank == 0 else None, dst=0, group=self.group)
-            stacked = self.stacked
+            dist.gather(tile, views if self.rank == 0 else None, dst=0, group=self.group)
         if self.rank != 0:
             return None
         if not assemble_frame:

@@ -48,6 +48,10 @@ class Renderer:
     def set_culling(self, enabled: bool) -> None:
         abi.check(self.lib.sr_debug_set_culling(self.ctx, 1 if enabled else 0), "sr_debug_set_culling")
 
+    def set_split(self, max_tiles: int, lanes_per_wave: int = 16, min_steps: int = 1) -> None:
+        """Run the costliest tiles of the previous frame as sparse waves (sr_set_split; 0 tiles: off)."""
+        abi.check(self.lib.sr_set_split(self.ctx, int(max_tiles), int(lanes_per_wave), int(min_steps)), "sr_set_split")
+
     # ---- rendering -------------------------------------------------------------
     def set_timing(self, capacity: int) -> None:
         """Record per-kernel HIP events for the next `capacity` frames (0: off)."""
@@ -60,6 +64,14 @@ class Renderer:
         abi.check(self.lib.sr_debug_kernel_times(self.ctx, buf, max_frames, C.byref(n)), "sr_debug_kernel_times")
         k = min(n.value, max_frames)
         return np.frombuffer(buf, dtype=np.float32, count=3 * k).reshape(k, 3).copy()
+
+    def last_order(self) -> np.ndarray:
+        """The launch codes the last frame left for the next one (tile << 8, | 0x80 | sub when split, -1 unused)."""
+        n = C.c_int()
+        abi.check(self.lib.sr_debug_last_order(self.ctx, None, 0, C.byref(n)), "sr_debug_last_order")
+        buf = (C.c_int * max(1, n.value))()
+        abi.check(self.lib.sr_debug_last_order(self.ctx, buf, n.value, C.byref(n)), "sr_debug_last_order")
+        return np.frombuffer(buf, dtype=np.int32, count=n.value).copy()
 
     def _stream(self, stream):
         if stream is None:
@@ -96,6 +108,26 @@ class Renderer:
                                       block_first, block_step, C.c_void_p(out.data_ptr()), width * 4,
                                       self._stream(stream)),
             "sr_render_blocks",
+        )
+        return out, rows
+
+    def render_blocks_batch(self, cams, params: abi.Params, width: int, height: int, block_rows: int,
+                            block_first: int, block_step: int, out=None, stream=None):
+        """sr_render_blocks' rows of len(cams) frames in one launch -> ([B, tile_rows, W, 4], rows)."""
+        rows = self.lib.sr_blocks_row_count(height, block_rows, block_first, block_step)
+        nblocks = -(-rows // block_rows) if rows else 0
+        cap = nblocks * block_rows
+        B = len(cams)
+        arr = (abi.Camera * B)(*cams)
+        if out is None:
+            out = self.torch.empty((B, cap, width, 4), dtype=self.torch.uint8, device=self.tdev)
+        assert out.is_contiguous() and out.dtype == self.torch.uint8 and tuple(out.shape[:1]) == (B,)
+        assert out[0].numel() >= cap * width * 4
+        abi.check(
+            self.lib.sr_render_blocks_batch(self.ctx, arr, B, C.byref(params), width, height, block_rows, block_first,
+                                            block_step, C.c_void_p(out.data_ptr()), width * 4,
+                                            out[0].numel(), self._stream(stream)),
+            "sr_render_blocks_batch",
         )
         return out, rows
 

@@ -54,10 +54,14 @@ def test_help_runs_without_a_gpu():
     assert r.returncode == 0 and "--workload" in r.stdout and "--inflight" in r.stdout
 
 
-def test_frames_in_flight_by_rank_share():
+def test_frames_per_launch_by_rank_share():
     import bench
 
-    # headline: 4 up to N = 4 (s12/s18 optimum per share), 6 at N = 8
-    assert [bench.frames_in_flight(1920, 1080, n) for n in (1, 2, 4, 8)] == [4, 4, 4, 6]
-    assert bench.frames_in_flight(640, 360, 1) == 6  # config 2
-    assert bench.frames_in_flight(3840, 2160, 1) == 4
+    # about four headline frames' worth of a rank's share per launch, 1..16
+    assert [bench.frames_per_launch(1920, 1080, n) for n in (1, 2, 4, 8)] == [4, 8, 16, 16]
+    assert bench.frames_per_launch(640, 360, 1) == 16  # config 2
+    assert bench.frames_per_launch(3840, 2160, 1) == 1 and bench.frames_per_launch(3840, 2160, 8) == 8
+    assert bench.frames_per_launch(7680, 4320, 8) == 2
+    assert bench.launches_in_flight(4) == 3 and bench.launches_in_flight(1) == 4
+    a = _parse(["--batch", "2", "--split", "32:4:1000"])
+    assert a.batch == 2 and a.split == "32:4:1000"

@@ -94,3 +94,63 @@ def test_assemble_numpy_matches_loop(pkg):
             stacked[r, k] = y
     frame = D.assemble(stacked, world, h, 8)
     assert frame[:, 0, 0].tolist() == list(range(h))
+
+
+def batch_worker(rank, world, port, q):
+    """Batched tiles [B, tile_rows, W, C] (sr_render_blocks_batch's layout):
+    frame b's row y holds (b, y); __call__(n) gathers the first n frames."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import srpkg
+
+    D = srpkg.load_package().dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, h = 5, 45
+        tile = torch.full((B, D.tile_rows(world, h, 8), 3, 2), -1, dtype=torch.int32)
+        for b in range(B):
+            for k, y in enumerate(D.rows_of(rank, world, h, 8)):
+                tile[b, k, :, 0] = b
+                tile[b, k, :, 1] = y
+        g = D.FrameGather(tile, world, rank, h, 8)
+        for n in (B, 3):
+            frames = g(n)
+            if rank == 0:
+                q.put((n, frames.numpy().copy()))
+            else:
+                assert frames is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_batched_gather_reassembles_frames(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=batch_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    for n, frames in got:
+        assert frames.shape == (n, 45, 3, 2)
+        for b in range(n):
+            assert (frames[b, :, :, 0] == b).all()
+            assert frames[b, :, 0, 1].tolist() == list(range(45))
+
+
+def test_assemble_batched_matches_per_frame(pkg):
+    D = pkg.dist
+    world, h, B = 4, 61, 3
+    rng = np.random.default_rng(0)
+    stacked = rng.integers(0, 255, (world, B, D.tile_rows(world, h, 8), 5, 4)).astype(np.uint8)
+    per = np.stack([D.assemble(stacked[:, b], world, h, 8) for b in range(B)])
+    assert np.array_equal(D.assemble(stacked, world, h, 8), per)
+    assert np.array_equal(D.assemble(torch.from_numpy(stacked), world, h, 8).numpy(), per)

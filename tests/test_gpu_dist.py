@@ -50,7 +50,7 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world):
                  "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(world),
                  "--dist-backend", "gloo"], tmp_path / "multi")
     assert multi["n_gpus"] == world and single["n_gpus"] == 1
-    assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["frames_in_flight"] == 3
+    assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["launches_in_flight"] == 3
     one = sorted((tmp_path / "one").glob("frame_*.npy"))
     many = sorted((tmp_path / "multi").glob("frame_*.npy"))
     assert len(one) == len(many) == 6

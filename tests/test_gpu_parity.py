@@ -175,6 +175,81 @@ def test_culling_is_exact(pkg, gpu, seed):
     assert np.array_equal(outs[0][2], outs[1][2])
 
 
+@pytest.mark.parametrize("lanes", [16, 4, 1])
+def test_split_tiles_bit_identical(pkg, gpu, lanes):
+    """Split tiles (sr_set_split) change which rays share a wave, never a
+    pixel: the costliest tiles of the previous frame, re-run as waves of 16,
+    4 or 1 rays, give the same float FragColor, RGBA8 and step counts as whole
+    tiles - full frames, a row band and a block-cyclic share."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    gpu.set_scene(sc.scene_default(textured=True))
+    gpu.set_test_ray(abi.default_test_ray())
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+
+    def frame(cam, W, H, rows):
+        f, b, s = gpu.render_debug(cam, params, W, H, *rows)
+        torch.cuda.synchronize()
+        return f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()
+
+    cases = [(abi.default_camera(), 480, 270, (0, None)), (sc.random_camera(7), 320, 200, (0, None)),
+             (abi.default_camera(), 640, 360, (96, 224))]
+    for cam, W, H, rows in cases:
+        gpu.set_split(0)
+        ref = frame(cam, W, H, rows)
+        gpu.set_split(24, lanes, 1)
+        frame(cam, W, H, rows)  # learns the tile costs (centre-out order, nothing split yet)
+        codes = gpu.last_order()
+        n_split = int(((codes >= 0) & ((codes & 0x80) != 0)).sum())
+        assert n_split == 24 * (64 // lanes), (n_split, codes[:8])
+        got = frame(cam, W, H, rows)  # runs the split launch
+        gpu.set_split(0)
+        for a, b_, what in zip(ref, got, ("float", "rgba8", "steps")):
+            assert np.array_equal(a, b_), f"{what} differs with split tiles ({lanes} lanes, {W}x{H} rows {rows})"
+    # the multi-GPU share path
+    cam = abi.default_camera()
+    gpu.set_split(0)
+    ref, rows = gpu.render_blocks(cam, params, 480, 270, 8, 1, 4)
+    ref = ref.cpu().numpy()
+    gpu.set_split(16, lanes, 1)
+    for _ in range(2):
+        got, _ = gpu.render_blocks(cam, params, 480, 270, 8, 1, 4)
+    gpu.set_split(0)
+    torch.cuda.synchronize()
+    assert np.array_equal(ref[:rows], got.cpu().numpy()[:rows])
+
+
+@pytest.mark.parametrize("split", [0, 12])
+def test_batch_equals_single_frames(pkg, gpu, split):
+    """sr_render_blocks_batch: B frames with different cameras (the flyby) in
+    one launch, byte-identical to rendering each frame alone - a whole frame
+    and a block-cyclic share, with and without split tiles."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    gpu.set_scene(sc.scene_default(textured=True))
+    gpu.set_test_ray(abi.default_test_ray())
+    params = abi.default_params(max_steps=1500, percent_black=-1.0)
+    W, H = 320, 184
+    for B, (first, step) in ((5, (0, 1)), (3, (1, 4)), (16, (2, 8))):
+        cams = [abi.camera_flyby((f + 0.5) / B, 30.0, 10.0) for f in range(B)]
+        gpu.set_split(0)
+        ref = []
+        for c in cams:
+            o, rows = gpu.render_blocks(c, params, W, H, 8, first, step)
+            ref.append(o.cpu().numpy()[:rows])
+        gpu.set_split(split, 4, 1)
+        for _ in range(2):  # the second batch runs the learned order (and split tiles)
+            out, rows = gpu.render_blocks_batch(cams, params, W, H, 8, first, step)
+        torch.cuda.synchronize()
+        gpu.set_split(0)
+        got = out.cpu().numpy()
+        assert len({r.tobytes() for r in ref}) == B  # every camera differs
+        for f in range(B):
+            assert np.array_equal(got[f, :rows], ref[f]), (B, first, step, f)
+
+
 def test_rows_and_blocks_assemble_full_frame(pkg, gpu):
     import torch
 
