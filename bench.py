@@ -471,11 +471,11 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
 
     The path is FP32-VALU bound (no contraction for MFMA, ~4 B of compulsory
     HBM traffic per pixel). `achieved` is the FP32 work the kernel EXECUTES:
-    the FLOP per launch counted by the hardware (SQ_INSTS_VALU_FLOPS_FP32 +
-    _TRANS, rocprofv3 --pmc on this kernel source and config, calibrated by
+    the FLOP per frame counted by the hardware (SQ_INSTS_VALU_FLOPS_FP32 +
+    _TRANS per integrate dispatch over the dispatch's B frames, rocprofv3
+    --pmc on this kernel source and config, calibrated by
     tools/microbench/flops_calib.hip: profiles/pmc_latest.json) times the
-    launches per second of this run (one per frame, F in flight), so `frac`
-    is utilisation of the FP32 peak. `kernel_ms` is the same run's mean
+    frames per second of this run, so `frac` is utilisation of the FP32 peak. `kernel_ms` is the same run's mean
     integrate-launch duration (HIP events on each launch's stream; a launch
     renders B frames and F launches overlap, `overlap` = kernel_ms / (B x
     ms_per_step)): it is what the rocprofv3 --stats summary of this command
@@ -485,16 +485,18 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
     executed = None
     achieved = None
     valu_issue = None
+    per_frame = (pmc or {}).get("frames_per_launch", 1)
     if pmc and pmc.get("flop_per_launch"):
-        executed = pmc["flop_per_launch"] * share
+        executed = pmc["flop_per_launch"] / per_frame * share  # per frame of this rank's share
         achieved = executed / (ms_per_step * 1e-3) / 1e12
         if pmc.get("valu_insts_per_launch"):
             # wave64 VALU instructions x 2 cycles on a SIMD-32 over the SIMD-cycles at 2.4 GHz
-            valu_issue = pmc["valu_insts_per_launch"] * share * 2.0 / (SIMDS * CLOCK_GHZ * 1e9 * ms_per_step * 1e-3)
+            valu_issue = (pmc["valu_insts_per_launch"] / per_frame * share * 2.0
+                          / (SIMDS * CLOCK_GHZ * 1e9 * ms_per_step * 1e-3))
     traffic = None
     tr = load_matching(args.traffic_json, W, H, N, world)
     if tr and world == 1:
-        traffic = tr.get("hbm_bytes_per_launch")
+        traffic = tr.get("hbm_bytes_per_frame", tr.get("hbm_bytes_per_launch"))
     hbm_bytes = rows_mine * W * 4  # compulsory RGBA8 store; textures stay cache resident
     ref_flop = sigma_steps_mine * FLOP_PER_STEP + rows_mine * W * FLOP_PER_PIXEL
     return {
@@ -505,7 +507,7 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
         "unit": "TFLOP/s",
         "frac": None if achieved is None else round(achieved / PEAK_FP32_TFLOPS, 4),
         "traffic": traffic,
-        "executed_flop_per_launch": None if executed is None else round(executed),
+        "executed_flop_per_frame": None if executed is None else round(executed),
         "valu_issue_frac": None if valu_issue is None else round(valu_issue, 4),
         "kernel_ms": round(integrate_ms, 4),
         "overlap": round(integrate_ms / (B * ms_per_step), 2),

@@ -82,6 +82,16 @@ def frame_counters(roots, kernel="sr_integrate_kernel<true>"):
     return frame_grid, {k: sum(v) / len(v) for k, v in per.items()}, {k: len(v) for k, v in per.items()}
 
 
+def frames_per_dispatch(grid_threads, width, height):
+    """Frames one integrate dispatch of a whole-frame grid renders: the grid is
+    B x (16x16 tiles) x 256 threads (sr_render_blocks_batch; split tiles off)."""
+    tiles = ((width + 15) // 16) * ((height + 15) // 16)
+    B, rem = divmod(int(grid_threads), tiles * 256)
+    if rem or B < 1:
+        raise SystemExit(f"grid of {grid_threads} threads is not a whole number of {width}x{height} frames")
+    return B
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calib", required=True)
@@ -119,6 +129,7 @@ def main():
           f"exec-mask blind: {mask_blind}; transcendentals inside FLOPS_FP32: {trans_in_fp32}; per TRANS unit {k_trans:.4g}")
 
     grid, c, n = frame_counters(args.frame)
+    B = frames_per_dispatch(grid, args.width, args.height)
     flop = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * k_flop  # transcendentals included (1 each)
     trans = c.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0) * k_trans
     rec = {
@@ -129,9 +140,12 @@ def main():
         "max_steps": args.max_steps,
         "grid_threads": grid,
         "dispatches_averaged": max(n.values()) if n else 0,
+        "frames_per_launch": B,
         "flop_per_launch": flop,
         "trans_ops_per_launch": trans,
         "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
+        "flop_per_frame": flop / B,
+        "valu_insts_per_frame": None if c.get("SQ_INSTS_VALU") is None else c["SQ_INSTS_VALU"] / B,
         "calibration": {"flop_per_unit": k_flop, "trans_per_unit": k_trans, "max_deviation": spread,
                         "exec_mask_blind": mask_blind, "trans_inside_fp32": trans_in_fp32},
         "counters": c,
@@ -143,7 +157,8 @@ def main():
         "source": args.source,
     }
     Path(args.out).write_text(json.dumps(rec, indent=1) + "\n")
-    print(json.dumps({k: rec[k] for k in ("flop_per_launch", "valu_insts_per_launch", "dispatches_averaged")}))
+    print(json.dumps({k: rec[k] for k in ("frames_per_launch", "flop_per_launch", "flop_per_frame",
+                                          "valu_insts_per_launch", "dispatches_averaged")}))
 
 
 if __name__ == "__main__":

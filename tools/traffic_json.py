@@ -17,7 +17,7 @@ from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from pmc_flops import frame_counters  # noqa: E402
+from pmc_flops import frame_counters, frames_per_dispatch  # noqa: E402
 
 
 def main():
@@ -30,7 +30,8 @@ def main():
     a = ap.parse_args()
     import bench
 
-    _, c, _ = frame_counters(a.frame)
+    grid, c, _ = frame_counters(a.frame)
+    B = frames_per_dispatch(grid, a.width, a.height)
     fetch = c["FETCH_SIZE"] * 1024.0
     write = c["WRITE_SIZE"] * 1024.0
     rec = {
@@ -39,6 +40,8 @@ def main():
         "width": a.width, "height": a.height, "max_steps": a.max_steps,
         "fetch_bytes_raw": fetch, "fetch_bytes_x2_bound": 2 * fetch, "write_bytes": write,
         "hbm_bytes_per_launch": fetch + write,
+        "frames_per_launch": B,
+        "hbm_bytes_per_frame": (fetch + write) / B,
         "note": "reads: scene/step table (scalar, cache-resident) + opacity map; writes: pixel-state planes "
                 "for the shade kernel (DESIGN.md §6); the algorithmic output is the shade kernel's 4 B/px store",
         "source": " ".join(a.frame),
