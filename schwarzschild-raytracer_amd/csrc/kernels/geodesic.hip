@@ -541,27 +541,41 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     budget_frame(sc, bs, nv, tv);
 }
 
+// The orbit's (pa, pb) on each budgeted cylinder's axis (budget_frame),
+// read from LDS once per fast loop: they change only at reseeds.
+struct CylDirs {
+    float pa[SR_MAX_CYLINDERS], pb[SR_MAX_CYLINDERS];
+};
+__device__ __forceinline__ CylDirs cyl_dirs(const sr_dev_scene* __restrict__ sc, const Budget& bs) {
+    CylDirs d;
+    uint32_t c = (uint32_t)sc->budget_cyl_mask;
+#pragma unroll
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        d.pa[k] = d.pb[k] = 0.0f;
+        if (c) {
+            d.pa[k] = bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE];
+            d.pb[k] = bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE];
+            c &= c - 1;
+        }
+    }
+    return d;
+}
+
 // Whether the chord with in-plane components (a, b) (chord = nv a + tv b, up
 // to perr absolute) may be closer than SR_BUDGET_DPMIN to a budgeted
 // cylinder's axis direction; bit k of the result: cylinder k (bit order of
 // budget_cyl_mask). Decided with twice the threshold and forced when the
-// direction is not known to 0.4%.
-__device__ __forceinline__ uint32_t chord_parallel(const sr_dev_scene* __restrict__ sc, const Budget& bs, float a,
-                                                   float b, float perr) {
-    const uint32_t cm = bs.cm;
-    uint32_t c = (uint32_t)sc->budget_cyl_mask;
+// direction is not known to 0.4%. Branch-free over the cylinder capacity
+// (unused slots have pa = pb = 0 and no bit in cm).
+__device__ __forceinline__ uint32_t chord_parallel(uint32_t cm, const CylDirs& cd, float a, float b, float perr) {
     const float dd = a * a + b * b;
     const bool vague = !(perr * perr <= 1.6e-5f * dd);
     uint32_t par = 0;
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
-        if (c) {
-            const float ca = a * bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE] +
-                             b * bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE];
-            const bool near = vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd);
-            par |= (uint32_t)near << k;
-            c &= c - 1;
-        }
+        const float ca = a * cd.pa[k] + b * cd.pb[k];
+        const bool near = vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd);
+        par |= (uint32_t)near << k;
     }
     return par & cm;
 }
@@ -1558,6 +1572,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             e = ldc(tp);
             float4 e1 = ldc(tp + 1);
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
+            const CylDirs cd = CM ? cyl_dirs(sc, bs) : CylDirs{};
+            // the LDS reads land before the loop: a wait for them inside it
+            // would also wait for the step table's prefetch (one counter)
+            if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             for (;;) {
                 // the next step's entry, loaded a step ahead (the table holds
                 // max_steps + 1 entries and i + 1 <= N)
@@ -1575,7 +1593,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
                     Tn = __builtin_fmaf(sq, e1.z, Tn);
                     if (CM) {
-                        par = chord_parallel(sc, bs, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
+                        par = chord_parallel(bs.cm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
                         lim = par ? nmin(lim0, bs.mh) : lim0;
                     }
                 }
