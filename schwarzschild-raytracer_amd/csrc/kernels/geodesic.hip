@@ -469,6 +469,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
+#ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries)
+#define SR_FAST_UNROLL 3
+#endif
 #ifndef SR_AHEAD_T
 #define SR_AHEAD_T 1.0f
 #endif
@@ -1576,11 +1579,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
             if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-            for (;;) {
-                // the next step's entry, loaded a step ahead (the table holds
-                // max_steps + 1 entries and i + 1 <= N)
-                const float4 en = ldc(tp + 2), e1n = ldc(tp + 3);
-                __builtin_amdgcn_sched_barrier(0);  // issued first: a step of latency to hide
+            // Step i from entry (e, e1): RK4, the chord-length bound and the
+            // exit test; true when some lane needs attention (the step is then
+            // computed but not applied).
+            auto compute = [&]() -> bool {
                 rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
                 rB = __builtin_amdgcn_rcpf(un);
                 Tn = bs.T;
@@ -1600,12 +1602,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
                 // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
-                if (__ballot(!(Tn < lim) || un < fr.u_f)) {
-                    // a use on the exit path keeps the prefetch where it is
-                    // issued (sunk into the latch it would wait at once)
-                    asm volatile("; keep %0 %1" ::"s"(en.x), "s"(e1n.x));
-                    break;
-                }
+                return __ballot(!(Tn < lim) || un < fr.u_f);
+            };
+            // apply step i and move to entry (en, en1) of step i + 1
+            auto apply = [&](float4 en, float4 en1) -> bool {
                 bs.T = Tn;
                 up = r.u;
                 r.u = un;
@@ -1614,8 +1614,33 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 tp += 2;
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
-                e1 = e1n;
-                if (++i >= N) break;
+                e1 = en1;
+                return ++i >= N;
+            };
+            // SR_FAST_UNROLL steps per iteration: the entries of steps i + 1
+            // .. i + SR_FAST_UNROLL are loaded together at its top (the table
+            // holds max_steps + 4 entries), so step i + 1 waits only for loads
+            // issued a step earlier, and the copies rename the registers one
+            // step would rotate. A use on each exit path keeps the loads where
+            // they are issued (sunk to their first use, they would be waited
+            // at once).
+            for (;;) {
+                float4 nx[2 * SR_FAST_UNROLL];
+#pragma unroll
+                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
+                __builtin_amdgcn_sched_barrier(0);
+                bool leave = false;
+#pragma unroll
+                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
+                    if (compute()) {
+#pragma unroll
+                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        leave = true;
+                    } else {
+                        leave = apply(nx[2 * k], nx[2 * k + 1]);
+                    }
+                }
+                if (leave) break;
             }
         };
         if (any_cm) fast(std::true_type{});

@@ -301,8 +301,8 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
     // lie within 4e-6 (r1 + r2) of the ideal ones, and r1 + r2 <= (2 / sqrt(g)
     // + 1) sqrt((r2 - r1)^2 + r1 r2 g) (min(r1, r2) <= sqrt(r1 r2)), so
     // K = (1.0001 + 4.01e-6 (2.001 / sqrt(g) + 1)) x path slack 1.01, rounded
-    // up, covers both. One padding entry.
-    std::vector<float4> h(2 * ((size_t)max_steps + 1), make_float4(0.f, 0.f, 0.f, 0.f));
+    // up, covers both. Four padding entries (the step loop loads up to four steps ahead).
+    std::vector<float4> h(2 * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
     double c1 = 1.0, s1 = 0.0;
     for (int i = 0; i < max_steps; i++) {
