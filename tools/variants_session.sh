@@ -1,7 +1,7 @@
 #!/bin/bash
 # Bench lines for the non-headline BASELINE.json configs and the SURVEY §8(f)
 # row-3 variants (split modes 2/3, noise mask 0.75, reference loop without
-# culling). One bench.py process per line, each under its own time limit;
+# culling), and the headline with single-frame launches and a flyby camera. One bench.py process per line, each under its own time limit;
 # a failure ends the session.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -16,6 +16,10 @@ run() {  # name timeout bench-args...
   grep '^{' "$OUT/$name.log" >> "$OUT/variants.jsonl"
   return $rc
 }
+run headline 180 --steps 20 --warmup 3 || exit $?
+run headline_b1 180 --batch 1 --inflight 4 --steps 20 --warmup 3 || exit $?
+run flyby 180 --camera flyby --steps 20 --warmup 3 || exit $?
+run flyby_b1 180 --camera flyby --batch 1 --inflight 4 --steps 20 --warmup 3 || exit $?
 run small 180 --workload small --steps 20 --warmup 3 || exit $?
 run 4k 240 --workload 4k --steps 5 --warmup 1 || exit $?
 run 8k 300 --workload 8k --steps 2 --warmup 1 || exit $?
