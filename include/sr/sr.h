@@ -82,7 +82,8 @@ typedef enum {
     SR_E_HIP = -3,       /* a HIP runtime call failed */
     SR_E_NOMEM = -4,     /* host or device allocation failed */
     SR_E_NOT_READY = -5, /* sr_render before sr_set_scene */
-    SR_E_NO_DEVICE = -6  /* no HIP device / bad device ordinal */
+    SR_E_NO_DEVICE = -6, /* no HIP device / bad device ordinal */
+    SR_E_IO = -7         /* a file could not be written (sr_write_png) */
 } sr_status;
 
 /* struct Transform — black_hole.frag:41-44 */
@@ -316,6 +317,14 @@ int sr_blocks_row_count(int height, int block_rows, int block_first, int block_s
 /* sizeof of the ABI structs, for binding checks: sr_camera, sr_params,
  * sr_scene, sr_test_ray, sr_material, sr_light (in that order). */
 int sr_abi_struct_sizes(size_t* out, int n);
+
+/* Presentation (not in the hot path): writes a frame in host memory as an
+ * RGBA8 PNG. Replaces the reference's window present (src/main.cpp:318-319
+ * draw, :432 glfwSwapBuffers) for offline use. Rows are read bottom-up as GL
+ * and sr_render leave them when flip_rows != 0 (row 0 = the image's bottom).
+ * SR_E_IO when the file cannot be written. */
+int sr_write_png(const char* path, const uint8_t* rgba8, int width, int height, size_t pitch_bytes,
+                 int flip_rows);
 
 /* Host-side press-R geodesic (src/main.cpp:94-124): writes up to max_points
  * xyz triples into out_xyz and the count into *out_count. */

@@ -38,6 +38,7 @@ SR_E_HIP = -3
 SR_E_NOMEM = -4
 SR_E_NOT_READY = -5
 SR_E_NO_DEVICE = -6
+SR_E_IO = -7
 
 F3 = C.c_float * 3
 F9 = C.c_float * 9
@@ -186,6 +187,7 @@ SIGNATURES = {
     "sr_render_debug": (_i, [_p, C.POINTER(Camera), C.POINTER(Params), _i, _i, _i, _i, _p, _p, _p, _p]),
     "sr_blocks_row_count": (_i, [_i, _i, _i, _i]),
     "sr_set_split": (_i, [_p, _i, _i, _i]),
+    "sr_write_png": (_i, [C.c_char_p, _p, _i, _i, C.c_size_t, _i]),
     "sr_render_blocks_batch": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, _i, _i, _p,
                                     C.c_size_t, C.c_size_t, _p]),
     "sr_abi_struct_sizes": (_i, [C.POINTER(C.c_size_t), _i]),
@@ -240,6 +242,18 @@ def status_string(status: int) -> str:
 def check(status: int, what: str) -> None:
     if status != SR_OK:
         raise SRError(status, what)
+
+
+def write_png(path, frame, flip_rows: bool = True) -> None:
+    """sr_write_png: an [H, W, 4] uint8 frame (host array; rows bottom-up as
+    sr_render leaves them when flip_rows) as an RGBA8 PNG."""
+    import numpy as np
+
+    a = np.ascontiguousarray(frame, dtype=np.uint8)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError(f"expected an [H, W, 4] frame, got {a.shape}")
+    h, w, _ = a.shape
+    check(load().sr_write_png(str(path).encode(), a.ctypes.data, w, h, w * 4, 1 if flip_rows else 0), "sr_write_png")
 
 
 def check_layout() -> dict:

@@ -563,6 +563,7 @@ const char* sr_status_string(int s) {
     case SR_E_NOMEM: return "out of memory";
     case SR_E_NOT_READY: return "scene not set";
     case SR_E_NO_DEVICE: return "no HIP device";
+    case SR_E_IO: return "file write failed";
     default: return "unknown status";
     }
 }

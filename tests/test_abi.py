@@ -222,3 +222,27 @@ def test_flyby_camera_follows_the_hyperbola(pkg):
     for c, p in ((c0, p0), (c5, p5), (c1, p1)):
         fwd = np.array(c.transform.axes[6:9], dtype=np.float64)
         assert np.allclose(fwd, -p / np.linalg.norm(p), atol=1e-5) and c.fov == 90.0
+
+
+def test_write_png_round_trip(pkg, tmp_path):
+    """sr_write_png (presentation): the PNG decodes (PIL) to the frame with
+    its bottom-up rows flipped, every filter path exercised by random, flat and
+    gradient rows; bad arguments and unwritable paths are rejected."""
+    PIL = pytest.importorskip("PIL.Image")
+    abi = pkg.abi
+    rng = np.random.default_rng(3)
+    h, w = 37, 53
+    frame = rng.integers(0, 256, (h, w, 4), dtype=np.uint8)
+    frame[5:9] = 7  # flat rows
+    frame[10:20] = (np.arange(w)[None, :, None] * 3 + np.arange(10)[:, None, None]).astype(np.uint8)
+    for flip in (True, False):
+        path = tmp_path / f"f{int(flip)}.png"
+        abi.write_png(path, frame, flip_rows=flip)
+        got = np.asarray(PIL.open(path).convert("RGBA"))
+        assert np.array_equal(got, frame[::-1] if flip else frame)
+    lib = abi.load()
+    buf = np.zeros((4, 4, 4), np.uint8)
+    assert lib.sr_write_png(None, buf.ctypes.data, 4, 4, 16, 1) == abi.SR_E_INVALID
+    assert lib.sr_write_png(b"x.png", buf.ctypes.data, 4, 4, 8, 1) == abi.SR_E_INVALID  # pitch < 4 w
+    assert lib.sr_write_png(str(tmp_path / "no" / "dir.png").encode(), buf.ctypes.data, 4, 4, 16, 1) == abi.SR_E_IO
+    assert lib.sr_status_string(abi.SR_E_IO) == b"file write failed"
