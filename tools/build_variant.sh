@@ -12,7 +12,8 @@ H=/opt/rocm/bin/hipcc
 $H $FLAGS --offload-arch=gfx950 -fno-gpu-rdc "$@" -x hip -c $PKG/csrc/kernels/geodesic.hip -o $OBJ/geodesic.o &
 $H $FLAGS "$@" -c $PKG/csrc/sr_api.cpp -o $OBJ/sr_api.o &
 $H $FLAGS -c $PKG/csrc/host/scene.cpp -o $OBJ/scene.o &
+$H $FLAGS -c $PKG/csrc/host/png.cpp -o $OBJ/png.o &
 wait
-$H -shared --offload-arch=gfx950 -Wl,-Bsymbolic -o $OUT/libsr_$NAME.so $OBJ/geodesic.o $OBJ/sr_api.o $OBJ/scene.o
+$H -shared --offload-arch=gfx950 -Wl,-Bsymbolic -o $OUT/libsr_$NAME.so $OBJ/geodesic.o $OBJ/sr_api.o $OBJ/scene.o $OBJ/png.o -lz
 $H $FLAGS --offload-arch=gfx950 "$@" -x hip --cuda-device-only -S $PKG/csrc/kernels/geodesic.hip -o $OBJ/geodesic.s
 echo "$NAME: $(grep -E '^\s+\.(vgpr_count|sgpr_count|vgpr_spill_count)' $OBJ/geodesic.s | head -3 | tr -s ' ' | tr '\n' ' ')"
