@@ -60,9 +60,13 @@ __device__ __forceinline__ float gmax(float x, float y) { return x < y ? y : x; 
 // binary64 function, rounded once to binary32
 __device__ __forceinline__ float t_sin(float x) { return (float)sin((double)x); }
 __device__ __forceinline__ float t_cos(float x) { return (float)cos((double)x); }
-__device__ __forceinline__ float t_asin(float x) { return (float)asin((double)x); }
-__device__ __forceinline__ float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
-__device__ __forceinline__ float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+// asin / atan2 / pow are called only by the shading kernels: out of line, the
+// binary64 code's registers do not add to the lighting's (sr_shade_kernel 215
+// -> 117 VGPRs, 2 -> 4 waves per SIMD: 0.104 -> 0.060 ms per headline frame,
+// profiles/r02/s7_shade_noinline.jsonl)
+__device__ __attribute__((noinline)) float t_asin(float x) { return (float)asin((double)x); }
+__device__ __attribute__((noinline)) float t_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ __attribute__((noinline)) float t_pow(float x, float y) { return (float)pow((double)x, (double)y); }
 
 __device__ __forceinline__ f3 ld3(const float* p) { return F3(p[0], p[1], p[2]); }
 __device__ __forceinline__ m3 ldm(const float* a) {

@@ -220,17 +220,21 @@ def test_split_tiles_bit_identical(pkg, gpu, lanes):
     assert np.array_equal(ref[:rows], got.cpu().numpy()[:rows])
 
 
-@pytest.mark.parametrize("split", [0, 12])
-def test_batch_equals_single_frames(pkg, gpu, split):
+@pytest.mark.parametrize("split,mode", [(0, 0), (12, 0), (0, 2)])
+def test_batch_equals_single_frames(pkg, gpu, split, mode):
     """sr_render_blocks_batch: B frames with different cameras (the flyby) in
     one launch, byte-identical to rendering each frame alone - a whole frame
-    and a block-cyclic share, with and without split tiles."""
+    and block-cyclic shares, with and without split tiles, and in the
+    half-width split mode with the noise mask."""
     import torch
 
     sc, abi = pkg.scenes, pkg.abi
     gpu.set_scene(sc.scene_default(textured=True))
     gpu.set_test_ray(abi.default_test_ray())
-    params = abi.default_params(max_steps=1500, percent_black=-1.0)
+    if mode:
+        params = abi.default_params(max_steps=1500, percent_black=0.6, raytrace_type=mode, curved_percentage=0.4)
+    else:
+        params = abi.default_params(max_steps=1500, percent_black=-1.0)
     W, H = 320, 184
     for B, (first, step) in ((5, (0, 1)), (3, (1, 4)), (16, (2, 8))):
         cams = [abi.camera_flyby((f + 0.5) / B, 30.0, 10.0) for f in range(B)]
