@@ -507,3 +507,24 @@ def test_reference_assets_frame(pkg, oracle):
         o = oracle.render(scene, cam, params, 480, 270, tex)
         print(compare((b.cpu().numpy(), f.cpu().numpy(), s.cpu().numpy()), o, label))
     r.close()
+
+
+def test_presentation_png_of_a_gpu_frame(pkg, gpu, tmp_path):
+    """Presentation: a frame rendered on the GPU, copied to
+    the host and written by sr_write_png decodes (PIL) to the same pixels,
+    top row first (sr_render's rows are bottom-up, as GL leaves them)."""
+    import torch
+
+    PIL = pytest.importorskip("PIL.Image")
+    sc, abi = pkg.scenes, pkg.abi
+    gpu.set_scene(sc.scene_default(textured=True))
+    gpu.set_test_ray(abi.default_test_ray())
+    params = abi.default_params(max_steps=800, percent_black=-1.0)
+    frame = gpu.render(abi.default_camera(), params, 200, 113)
+    torch.cuda.synchronize()
+    frame = frame.cpu().numpy()
+    path = tmp_path / "frame.png"
+    abi.write_png(path, frame)
+    got = np.asarray(PIL.open(path).convert("RGBA"))
+    assert got.shape == (113, 200, 4)
+    assert np.array_equal(got, frame[::-1])

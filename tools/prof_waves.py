@@ -59,6 +59,11 @@ def main():
     out["cycles_by_section_all_waves"] = {k: int(v) for k, v in zip(SECTIONS, sums)}
     out["cycles_total_all_waves"] = int(total[ok].sum())
     out["reanchors_by_slot_all_waves"] = [int(v) for v in t[ok, 8:16].sum(0)]
+    out["events_all_waves"] = int(t[ok, 16].sum())
+    out["slow_entries_all_waves"] = int(t[ok, 19].sum())
+    out["phase1_ballots_all_waves"] = int(t[ok, 20].sum())
+    out["tail_top_all_waves"] = int(t[ok, 21].sum())
+    out["unaccounted_cycles_all_waves"] = int(total[ok].sum() - sums.sum() - t[ok, 20].sum() - t[ok, 21].sum())
     gx = (1920 + 15) // 16
     top = np.argsort(-total)[: args.top]
     out["slowest"] = [
