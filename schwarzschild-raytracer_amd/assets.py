@@ -6,11 +6,14 @@ array of `loadTextureArray` (image_utils.cpp:42-117) as the app loads them
 The files under `assets/textures/` are data copied unchanged from the
 reference's `assets/textures/` (see its sources.txt), so the GPU box, which
 has no /root/reference, renders the real inputs. Decoding: the reference uses
-stb_image v2.30 (image_utils.cpp:4-5), which is not importable here; PIL
-decodes instead. cubemap.png is lossless, so its texels equal stb_image's;
-the JPEGs may differ from stb_image's IDCT in the last bit of some texels
-(parity is GPU vs oracle on the same decoded texels, so that only moves the
-inputs, not the comparison). The decoded images are flipped vertically as
+stb_image (image_utils.cpp:4-5, 22-23). PIL decodes here, and the bytes where
+its JPEG IDCT differs from stb_image's (a few per ten thousand in the
+skyboxes, 5 % of uv_checker's; none in cubemap.png) are replaced from
+`assets/textures/stb_corrections.npz`, which tools/make_stb_corrections.py
+made with the reference's own stb_image: the decoded texels are stb_image's,
+byte for byte (tests/test_assets_stb.py). Both hashes are checked; if this
+machine's PIL decodes differently, the PIL texels are used with a warning.
+The decoded images are flipped vertically as
 `stbi_set_flip_vertically_on_load(true)` (image_utils.cpp:22) leaves them:
 row 0 = v 0, the bottom of the picture.
 """
@@ -28,19 +31,44 @@ SKYBOX = {"2k": TEXTURES / "background" / "2k.jpg", "8k": TEXTURES / "background
 ARRAY = [TEXTURES / "uv_checker.jpg", TEXTURES / "cubemap.png"]
 
 
+CORRECTIONS = TEXTURES / "stb_corrections.npz"
+
+
 def available() -> bool:
     return all(p.exists() for p in [*SKYBOX.values(), *ARRAY])
 
 
-def decode(path: Path) -> np.ndarray:
-    """stbi_load(path, ..., 0) with the vertical flip: uint8 [h, w, channels],
-    channels as stored (3 for the JPEGs, 4 for cubemap.png)."""
+def decode_pil(path: Path) -> np.ndarray:
+    """PIL's decode with the vertical flip: uint8 [h, w, channels], channels
+    as stored (3 for the JPEGs, 4 for cubemap.png)."""
     from PIL import Image
 
     with Image.open(path) as im:
         mode = {"RGB": "RGB", "RGBA": "RGBA", "L": "RGB", "P": "RGBA", "LA": "RGBA"}.get(im.mode, "RGB")
         a = np.asarray(im.convert(mode), dtype=np.uint8)
     return np.ascontiguousarray(a[::-1])
+
+
+def decode(path: Path) -> np.ndarray:
+    """stbi_load(path, ..., 0) with the vertical flip (image_utils.cpp:22-23):
+    PIL's decode with stb_image's bytes restored where they differ."""
+    import hashlib
+    import sys
+
+    a = decode_pil(path)
+    if not CORRECTIONS.exists():
+        return a
+    with np.load(CORRECTIONS) as c:
+        key = Path(path).name
+        if f"{key}/idx" not in c.files:
+            return a
+        if tuple(c[f"{key}/shape"]) != a.shape or hashlib.sha256(a.tobytes()).digest() != c[f"{key}/sha_pil"].tobytes():
+            print(f"assets: PIL decodes {key} differently here; using PIL's texels, not stb_image's", file=sys.stderr)
+            return a
+        flat = a.reshape(-1)
+        flat[c[f"{key}/idx"]] = c[f"{key}/val"]
+        assert hashlib.sha256(a.tobytes()).digest() == c[f"{key}/sha_stb"].tobytes(), key
+    return a
 
 
 def skybox(quality: str = "2k") -> np.ndarray:
