@@ -398,7 +398,7 @@ def main():
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             cpu = cpu_baseline(cams[0], W, H, N, args.cpu_sample_rows)
-        tex_desc = (f"the reference's assets/textures ({quality} skybox, uv_checker, cubemap; PIL-decoded)"
+        tex_desc = (f"the reference's assets/textures ({quality} skybox, uv_checker, cubemap; decoded to stb_image's bytes)"
                     if use_assets else f"procedural stand-in textures ({quality} skybox)")
         line = {
             "metric": ("Mpixels/s at 1920x1080, 2000 geodesic steps; 1/2/4/8 MI355X"
