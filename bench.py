@@ -66,7 +66,8 @@ FLYBY = (30.0, 10.0)  # src/main.cpp:409: hyperbolicTrajectory(30, 10, t)
 
 
 HEADLINE_PX = 1920 * 1080
-MAX_BATCH = 16  # SR_MAX_BATCH (sr_render_blocks_batch)
+MAX_BATCH = 16  # the bench's cap (the library takes SR_MAX_BATCH = 32): at N = 8, 16 and 20 frames per
+# launch measured the same over the 20-frame window (profiles/r02/s10_batch32_k20.jsonl)
 
 
 def frames_per_launch(width, height, world):

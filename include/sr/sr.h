@@ -290,7 +290,7 @@ int sr_render_blocks(sr_ctx* ctx, const sr_camera* cam, const sr_params* params,
  * frame_stride_bytes. One launch carries n_frames times the work, so a GPU
  * holding a small share of each frame (multi-GPU row tiling) runs it as
  * efficiently as a whole frame; the launch order and split tiles follow the
- * costliest tiles over the batch. SR_E_CAPACITY above 16 frames. */
+ * costliest tiles over the batch. SR_E_CAPACITY above 32 frames. */
 int sr_render_blocks_batch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params,
                            int width, int height, int block_rows, int block_first, int block_step,
                            uint8_t* dev_rgba8, size_t pitch_bytes, size_t frame_stride_bytes, sr_stream stream);

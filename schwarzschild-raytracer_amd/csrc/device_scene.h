@@ -137,7 +137,7 @@ typedef struct {
 
 // Frames one launch renders (sr_render_blocks_batch): the same rows of
 // `batch` frames that differ only in the camera.
-#define SR_MAX_BATCH 16
+#define SR_MAX_BATCH 32
 
 // Per-launch constants (kernel argument, scalar-loaded).
 typedef struct {

@@ -466,10 +466,22 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // spent are re-anchored (and tested if the chord may reach them). Unused
 // slots hold +inf. (pa, pb)[k] = (nv, tv) . axis of the k-th budgeted
 // cylinder (budget_cyl_mask bit order) for the chord-direction test.
-// E lives in LDS, one column per thread (E[j * 256], conflict-free): the
+// E lives in LDS, one column per thread (E[j * SR_WG], conflict-free): the
 // event loop indexes it with the wave-uniform slot j in a compact runtime
 // loop, and the step loop's registers hold only T and m.
-#define SR_E_STRIDE 256
+// SR_WG: threads per workgroup of the integrate and resume kernels (64, 128
+// or 256: one, two or four of a 16x16 tile's 8x8 waves). A workgroup's LDS
+// (72 B per thread) is held until its last wave ends: with 256-thread
+// workgroups a CU fills up with tiles whose one long wave runs on beside
+// three finished ones (busy wave slots 0.84 of the chip's over a headline
+// launch); one wave per workgroup frees each slot as its wave ends (0.94):
+// 1.27 -> 1.22 ms per headline frame, 1/8 share 0.185 -> 0.171
+// (profiles/r02/s10_wg_*).
+#ifndef SR_WG
+#define SR_WG 64
+#endif
+#define SR_WG_PER_TILE (256 / SR_WG)
+#define SR_E_STRIDE SR_WG
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
@@ -1799,22 +1811,26 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
     return quad * 64 + y8 * 8 + x8;
 }
 
-// 1-D grid: workgroup s renders launch code order[s / B] of frame s % B of
-// the batch (costliest tiles of every frame first, sr_order_kernel), and
-// records the tile's cost (max steps of its rays over the batch).
+// 1-D grid: workgroup s = (slot * B + f) * SR_WG_PER_TILE + part renders
+// part `part` (SR_WG threads) of launch code order[slot] of frame f of the
+// batch (costliest tiles of every frame first, sr_order_kernel), and records
+// the tile's cost (max steps of its rays over the batch).
 template <bool CULL>
-__global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
+__global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
     size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
     const unsigned B = (unsigned)fr.batch;
-    const int frame = B > 1 ? (int)(blockIdx.x % B) : 0;
-    const unsigned slot = B > 1 ? blockIdx.x / B : blockIdx.x;
+    const unsigned bid = blockIdx.x;
+    const unsigned wg = bid / SR_WG_PER_TILE;  // the tile's workgroup index (slot * B + f)
+    const int frame = B > 1 ? (int)(wg % B) : 0;
+    const unsigned slot = B > 1 ? wg / B : wg;
     const int code = order ? order[slot] : ((int)slot << 8);
     if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
     if (code < 0) return;  // unused slot of a split grid
     const int block = code >> 8;
-    const int tid = (code & SR_SPLIT) ? split_thread(code & 0x3f, (int)threadIdx.x, fr.split_log2) : (int)threadIdx.x;
+    const int ttid = (int)(bid % SR_WG_PER_TILE) * SR_WG + (int)threadIdx.x;  // thread of the tile's 256
+    const int tid = (code & SR_SPLIT) ? split_thread(code & 0x3f, ttid, fr.split_log2) : ttid;
 #ifndef SR_PRIO_BLOCKS
 #define SR_PRIO_BLOCKS 256
 #endif
@@ -1823,9 +1839,9 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     // than the rest of the grid. Raised issue priority keeps them near their
     // own latency bound while the other waves fill the idle issue slots.
 #ifdef SR_PRIO_SPLIT
-    if (order && ((code & SR_SPLIT) || blockIdx.x < SR_PRIO_BLOCKS)) __builtin_amdgcn_s_setprio(3);
+    if (order && ((code & SR_SPLIT) || wg < SR_PRIO_BLOCKS)) __builtin_amdgcn_s_setprio(3);
 #else
-    if (order && blockIdx.x < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
+    if (order && wg < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
 #endif
 #ifdef SR_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -1835,7 +1851,7 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     Pix q;
     int steps = 0;
 #ifdef SR_PROF
-    __shared__ unsigned prof_lds[4][SR_PROF_N];
+    __shared__ unsigned prof_lds[SR_WG / 64][SR_PROF_N];
     if ((threadIdx.x & 63) < SR_PROF_N) prof_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     const unsigned long long prof_t0 = clock64();
 #endif
@@ -1889,7 +1905,7 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
             rcm[j] = rcv[j];
             for (int off = 32; off > 0; off >>= 1) rcm[j] = max(rcm[j], __shfl_xor(rcm[j], off));
         }
-        const int w = block * 4 + (int)(threadIdx.x >> 6);
+        const int w = (frame * fr.tiles + block) * 4 + (ttid >> 6);
         if ((threadIdx.x & 63) == 0 && w < SR_WAVE_LOG) {
             unsigned long long* rec = sr_wave_t + (size_t)SR_WAVE_REC * w;
             rec[0] = t_start;
@@ -1897,12 +1913,14 @@ __global__ __launch_bounds__(256, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
             rec[2] = (unsigned long long)sm;
             rec[3] = em;
             for (int j = 0; j <= SR_MAX_BUDGET; j++) rec[4 + j] = (unsigned long long)rcm[j];
+            rec[13] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+            rec[14] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (wave, SIMD, CU, SE)
         }
     }
 #endif
 #ifdef SR_PROF
     {
-        const int w = block * 4 + (int)(threadIdx.x >> 6);
+        const int w = block * 4 + (ttid >> 6);
         int sm = steps;
         for (int off = 32; off > 0; off >>= 1) sm = max(sm, __shfl_xor(sm, off));
         if ((threadIdx.x & 63) == 0 && w < (1 << 17)) {
@@ -2020,7 +2038,7 @@ __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __res
 }
 
 template <bool CULL>
-__global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __restrict__ sc,
+__global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __restrict__ sc,
                                                        const float4* __restrict__ tbl,
                                                        const float* __restrict__ segs,
                                                        const uint32_t* __restrict__ bg,
@@ -2035,7 +2053,7 @@ __global__ __launch_bounds__(256) void sr_resume_kernel(const sr_dev_scene* __re
     tx.bg = bg;
     tx.arr = arr;
     tx.opq = nullptr;
-    for (int w = blockIdx.x * 256 + threadIdx.x; w < total; w += gridDim.x * 256) {
+    for (int w = blockIdx.x * SR_WG + threadIdx.x; w < total; w += gridDim.x * SR_WG) {
         const int id = list[w];
         const int f = (id >> 8) / fr.tiles;
         Pix q;
@@ -2094,21 +2112,21 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (cull)
-        hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B), block, 0, stream, sc, tbl, segs, arr, opq,
-                           *fr, ps, ps_n, count, order, cost);
+        hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
+                           tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else
-        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(slots * B), block, 0, stream, sc, tbl, segs, arr, opq,
-                           *fr, ps, ps_n, count, order, cost);
+        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
+                           tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
     hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
                        out, pitch, dbg_rgba, dbg_steps, list, count);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
-    unsigned nb = nblocks * B < 1024u ? nblocks * B : 1024u;
+    unsigned nb = (nblocks * B < 1024u ? nblocks * B : 1024u) * SR_WG_PER_TILE;
     if (cull)
-        hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
+        hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     else
-        hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), block, 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
+        hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     if (order)
         hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(1024), 0, stream, cost, (int)nblocks, fr->max_steps, order,

@@ -374,6 +374,11 @@ int ensure_pixel_state(sr_ctx* ctx, size_t n) {
         free_pixel_state(ctx);
         return SR_E_NOMEM;
     }
+    // [0]: the shade kernel's resume queue
+    if (!hip_ok(hipMemset(ctx->d_count, 0, 2 * sizeof(int)))) {
+        free_pixel_state(ctx);
+        return SR_E_HIP;
+    }
     ctx->ps_n = n;
     return SR_OK;
 }

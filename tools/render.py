@@ -56,8 +56,8 @@ def main():
     else:
         n = args.flyby
         cams = [abi.camera_flyby((f + 0.5) / n, 30.0, 10.0) for f in range(n)]
-        for first in range(0, n, 16):  # sr_render_blocks_batch takes up to 16 frames
-            out, rows = r.render_blocks_batch(cams[first:first + 16], params, W, H, H, 0, 1)
+        for first in range(0, n, 32):  # sr_render_blocks_batch takes up to 32 frames
+            out, rows = r.render_blocks_batch(cams[first:first + 32], params, W, H, H, 0, 1)
             torch.cuda.synchronize()
             for k, fr in enumerate(out.cpu().numpy()):
                 path = args.out % (first + k) if "%" in args.out else f"{Path(args.out).stem}_{first + k:03d}.png"
