@@ -66,18 +66,24 @@ FLYBY = (30.0, 10.0)  # src/main.cpp:409: hyperbolicTrajectory(30, 10, t)
 
 
 HEADLINE_PX = 1920 * 1080
-MAX_BATCH = 16  # the bench's cap (the library takes SR_MAX_BATCH = 32): at N = 8, 16 and 20 frames per
-# launch measured the same over the 20-frame window (profiles/r02/s10_batch32_k20.jsonl)
+MAX_BATCH = 16  # the bench's cap (the library takes SR_MAX_BATCH = 32)
 
 
-def frames_per_launch(width, height, world):
+def frames_per_launch(width, height, world, steps=None):
     """Default frames per launch (sr_render_blocks_batch): a rank's share of B
-    frames, B chosen so that one launch carries about four headline frames'
+    frames, B chosen so that one launch carries about eight headline frames'
     worth of pixels, 1..16. A rank holding 1/N of a frame then runs launches
     as large as a whole frame's: its share alone is latency-bound (the photon
-    ring's waves) and small concurrent launches fill the GPU badly
-    (profiles/r02/s3_batch_*.jsonl)."""
-    return max(1, min(MAX_BATCH, round(4 * HEADLINE_PX * world / (width * height))))
+    ring's waves) and small concurrent launches fill the GPU badly. With a
+    timed window of `steps` frames, at most half of it per launch: two
+    launches in flight overlap each other's ring-wave tails, one cannot
+    (profiles/r02/s3_batch_*.jsonl, s12_batch_k20.jsonl: over
+    20 frames, 8 / 10 / 10 / 10 frames per launch at N = 1 / 2 / 4 / 8 are
+    within 0.5 % of the best measured)."""
+    b = max(1, min(MAX_BATCH, round(8 * HEADLINE_PX * world / (width * height))))
+    if steps:
+        b = max(1, min(b, -(-steps // 2)))
+    return b
 
 
 def launches_in_flight(batch):
@@ -155,7 +161,7 @@ def main():
     distributed = world > 1
     W0, H0, N0 = WORKLOADS[args.workload]
     W, H, N = args.width or W0, args.height or H0, args.max_steps or N0
-    B = args.batch if args.batch > 0 else frames_per_launch(W, H, world)
+    B = args.batch if args.batch > 0 else frames_per_launch(W, H, world, args.steps)
     if not 1 <= B <= MAX_BATCH:
         raise SystemExit(f"bench: --batch must be 1..{MAX_BATCH}")
     F = args.inflight if args.inflight > 0 else launches_in_flight(B)

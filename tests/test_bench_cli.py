@@ -57,11 +57,14 @@ def test_help_runs_without_a_gpu():
 def test_frames_per_launch_by_rank_share():
     import bench
 
-    # about four headline frames' worth of a rank's share per launch, 1..16
-    assert [bench.frames_per_launch(1920, 1080, n) for n in (1, 2, 4, 8)] == [4, 8, 16, 16]
+    # about eight headline frames' worth of a rank's share per launch, 1..16
+    assert [bench.frames_per_launch(1920, 1080, n) for n in (1, 2, 4, 8)] == [8, 16, 16, 16]
+    # at most half of the timed window per launch (two launches overlap their tails)
+    assert [bench.frames_per_launch(1920, 1080, n, 20) for n in (1, 2, 4, 8)] == [8, 10, 10, 10]
+    assert bench.frames_per_launch(1920, 1080, 1, 5) == 3 and bench.frames_per_launch(1920, 1080, 1, 1) == 1
     assert bench.frames_per_launch(640, 360, 1) == 16  # config 2
-    assert bench.frames_per_launch(3840, 2160, 1) == 1 and bench.frames_per_launch(3840, 2160, 8) == 8
-    assert bench.frames_per_launch(7680, 4320, 8) == 2
+    assert bench.frames_per_launch(3840, 2160, 1) == 2 and bench.frames_per_launch(3840, 2160, 8) == 16
+    assert bench.frames_per_launch(7680, 4320, 1) == 1 and bench.frames_per_launch(7680, 4320, 8) == 4
     assert bench.launches_in_flight(4) == 3 and bench.launches_in_flight(1) == 4
     a = _parse(["--batch", "2", "--split", "32:4:1000"])
     assert a.batch == 2 and a.split == "32:4:1000"
