@@ -131,10 +131,14 @@ def parse():
                     help="launches in flight per GPU, each on its own context and stream (0: 3 for batched "
                          "launches, 4 for single frames)")
     ap.add_argument("--batch", type=int, default=0,
-                    help="frames per launch, 1..16 (sr_render_blocks_batch; 0: about four headline frames' worth "
-                         "of pixels of this rank's share per launch)")
+                    help="frames per launch, 1..16 (sr_render_blocks_batch; 0: about eight headline frames' worth "
+                         "of pixels of this rank's share per launch, at most half of --steps)")
     ap.add_argument("--split", default="0",
                     help="split tiles MAX_TILES[:LANES[:MIN_STEPS]] (sr_set_split; 0: off)")
+    ap.add_argument("--balance", choices=["cost", "cyclic"], default="cost",
+                    help="N > 1: cost: each rank renders an equal number of 8-row blocks of about equal cost "
+                         "(dist.balanced_blocks over the frame's step map, sr_render_block_list); cyclic: block b "
+                         "on rank b %% N")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl: RCCL gather of device tiles over xGMI (one GPU per rank); gloo: tiles staged "
                          "through host memory (ranks may share a GPU)")
@@ -248,9 +252,14 @@ def main():
                 if first + i >= dump_from[0]:
                     frames[first + i] = batch[i].clone()  # on the launch's stream (nccl) or host (gloo)
 
+    lists = [None]  # balanced_blocks lists (N > 1, --balance cost), set below from the step map
+
     def render(rk, first, n, out, s_k):
         """frames first .. first + n - 1 of this rank's share into out[:n]"""
-        if n == 1:
+        if lists[0] is not None:
+            rk.render_block_list(cams[first:first + n], params, W, H, BLOCK_ROWS, lists[0][rank], out=out[:n],
+                                 stream=s_k)
+        elif n == 1:
             rk.render_blocks(cams[first], params, W, H, BLOCK_ROWS, rank, world, out=out[0], stream=s_k)
         else:
             rk.render_blocks_batch(cams[first:first + n], params, W, H, BLOCK_ROWS, rank, world, out=out[:n],
@@ -286,9 +295,22 @@ def main():
             c[3].synchronize()
 
     # executed steps of this rank's rows (untimed; the debug variant of the kernel)
-    rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
     _, _, steps_full = r.render_debug(cams[0], params, W, H)
     torch.cuda.synchronize(dev)
+    balance = None
+    if distributed and args.balance == "cost":
+        # every rank derives the same lists from the same (bit-exact) step map
+        costs = D.wave_costs(steps_full, BLOCK_ROWS)
+        lists[0] = D.balanced_blocks(costs, world)
+        for c in ctxs:
+            c[2].lists = lists[0]
+        loads = [sum(costs[b] for b in l if b >= 0) for l in lists[0]]
+        cyc = [sum(costs[b] for b in D.blocks_of(k, world, H, BLOCK_ROWS)) for k in range(world)]
+        balance = {"max_over_mean": round(max(loads) / (sum(loads) / world), 4),
+                   "cyclic_max_over_mean": round(max(cyc) / (sum(cyc) / world), 4)}
+        rows_mine = D.rows_of_list(lists[0][rank], H, BLOCK_ROWS)
+    else:
+        rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
     sigma_steps_frame = int(steps_full.sum().item())
     sigma_steps_mine = int(steps_full[rows_mine].sum().item())
     # candidate critical bands: the 16-row bands of workgroup tiles holding the
@@ -433,8 +455,10 @@ def main():
                 "camera": args.camera,
                 "textures": "assets" if use_assets else "standin",
                 "skybox": quality,
-                "tiling": (f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), "
+                "tiling": ((f"cost-balanced {BLOCK_ROWS}-row blocks over {world} ranks (wave-cost map of the first "
+                            "frame), " if balance else f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), ")
                            + ("RCCL gather to rank 0" if not gloo else "gloo gather of host-staged tiles to rank 0")),
+                "balance": balance,
                 "dist_backend": args.dist_backend if distributed else None,
                 "launches_in_flight": F,
                 "frames_per_launch": B,

@@ -285,7 +285,7 @@ int sr_render_blocks(sr_ctx* ctx, const sr_camera* cam, const sr_params* params,
                      uint8_t* dev_rgba8, size_t pitch_bytes, sr_stream stream);
 
 /* Frames in one launch (not in the reference; the pixels are unchanged): the
- * rows sr_render_blocks would render, for n_frames (1 .. 16) frames that
+ * rows sr_render_blocks would render, for n_frames (1 .. 32) frames that
  * differ only in the camera (cams[f]), frame f packed at dev_rgba8 + f *
  * frame_stride_bytes. One launch carries n_frames times the work, so a GPU
  * holding a small share of each frame (multi-GPU row tiling) runs it as
@@ -294,6 +294,17 @@ int sr_render_blocks(sr_ctx* ctx, const sr_camera* cam, const sr_params* params,
 int sr_render_blocks_batch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params,
                            int width, int height, int block_rows, int block_first, int block_step,
                            uint8_t* dev_rgba8, size_t pitch_bytes, size_t frame_stride_bytes, sr_stream stream);
+
+/* A rank's cost-balanced rows (not in the reference; the pixels are
+ * unchanged): like sr_render_blocks_batch, but output row k of each frame's
+ * tile renders frame row blocks[k / block_rows] * block_rows + k % block_rows
+ * for an explicit list of n_blocks block indices (-1: padding, rows left
+ * unwritten). The list is copied to the device once per distinct list and
+ * kept with the context. schwarzschild-raytracer_amd/dist.py balanced_blocks
+ * builds equal-length lists of about equal cost for the ranks of a node. */
+int sr_render_block_list(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params, int width,
+                         int height, int block_rows, const int* blocks, int n_blocks, uint8_t* dev_rgba8,
+                         size_t pitch_bytes, size_t frame_stride_bytes, sr_stream stream);
 
 /* Debug/parity variant: unclamped FragColor as float RGBA (dev_rgba32, may be
  * NULL), the RGBA8 pixel (dev_rgba8, may be NULL) and the number of executed

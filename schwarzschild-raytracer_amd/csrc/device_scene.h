@@ -163,6 +163,9 @@ typedef struct {
     int32_t row_base;
     int32_t block_rows;
     int32_t block_stride;
+    // or, when block_list is set (sr_render_block_list): output row k renders
+    //   y = block_list[k / block_rows] * block_rows + (k % block_rows), none for -1
+    const int32_t* block_list;
     // textures (RGBA8 texels)
     int32_t bg_w, bg_h;
     int32_t arr_w, arr_h, arr_layers;

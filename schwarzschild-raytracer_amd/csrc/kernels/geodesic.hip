@@ -1320,7 +1320,13 @@ __device__ __forceinline__ bool pixel_of(const sr_dev_frame& fr, int block, int 
     q.px = bx * 16 + (wave & 1) * 8 + (lane & 7);
     q.k = by * 16 + (wave >> 1) * 8 + (lane >> 3);
     if (q.px >= fr.width || q.k >= fr.nrows) return false;
-    q.py = fr.row_base + (q.k / fr.block_rows) * fr.block_stride + (q.k % fr.block_rows);
+    if (fr.block_list) {  // sr_render_block_list: a rank's cost-balanced blocks
+        const int b = fr.block_list[q.k / fr.block_rows];
+        if (b < 0) return false;
+        q.py = b * fr.block_rows + (q.k % fr.block_rows);
+    } else {
+        q.py = fr.row_base + (q.k / fr.block_rows) * fr.block_stride + (q.k % fr.block_rows);
+    }
     return q.py < fr.height;
 }
 

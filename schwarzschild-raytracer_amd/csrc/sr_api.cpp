@@ -12,6 +12,7 @@
 #include <cstring>
 #include <map>
 #include <new>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -63,7 +64,10 @@ struct sr_ctx {
         int* order = nullptr;
         int* cost = nullptr;
     };
-    std::map<std::array<int, 4>, Order> orders;  // (gx, gy, split_tiles, split_log2)
+    // (gx, gy, split_tiles, split_log2, block list): a block list's tiles have their own costs
+    std::map<std::tuple<int, int, int, int, const int*>, Order> orders;
+    // device copies of the block lists of sr_render_block_list, by content
+    std::map<std::vector<int>, int*> block_lists;
     // split tiles (sr_set_split): 0 = off
     int split_tiles = 0, split_log2 = 4, split_min_steps = 1;
     const int* last_order = nullptr;  // the launch codes of the context's last frame (its next frame's order)
@@ -426,9 +430,9 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
 // buffer pair per shape and split setting, allocated on first use. Entries
 // are launch codes (geodesic.hip sr_order_kernel): tile << 8 for a whole
 // tile, -1 for the split grid's slots no tile uses yet.
-int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
+int ensure_order(sr_ctx* ctx, int gx, int gy, const int* list, int** order, int** cost) {
     const int split = ctx->split_tiles;
-    const std::array<int, 4> key{gx, gy, split, split ? ctx->split_log2 : 0};
+    const auto key = std::make_tuple(gx, gy, split, split ? ctx->split_log2 : 0, list);
     auto it = ctx->orders.find(key);
     if (it != ctx->orders.end()) {
         *order = it->second.order;
@@ -461,6 +465,30 @@ int ensure_order(sr_ctx* ctx, int gx, int gy, int** order, int** cost) {
     ctx->orders[key] = o;
     *order = o.order;
     *cost = o.cost;
+    return SR_OK;
+}
+
+// The device copy of a block list (sr_render_block_list), uploaded once per
+// distinct list on the caller's stream and kept for the context's lifetime (a
+// rank's balanced list does not change between frames).
+int ensure_block_list(sr_ctx* ctx, const int* blocks, int n, hipStream_t s, const int** dev) {
+    std::vector<int> key(blocks, blocks + n);
+    auto it = ctx->block_lists.find(key);
+    if (it != ctx->block_lists.end()) {
+        *dev = it->second;
+        return SR_OK;
+    }
+    int* d = nullptr;
+    if (!hip_ok(hipMalloc(&d, (size_t)n * sizeof(int)))) return SR_E_NOMEM;
+    // ordered before this context's launches on its stream; synchronized once
+    // so that the host copy of the list may go
+    if (!hip_ok(hipMemcpyAsync(d, key.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, s)) ||
+        !hip_ok(hipStreamSynchronize(s))) {
+        (void)hipFree(d);
+        return SR_E_HIP;
+    }
+    ctx->block_lists[std::move(key)] = d;
+    *dev = d;
     return SR_OK;
 }
 
@@ -509,7 +537,8 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
 // frame_stride) in one launch of each kernel.
 int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params, int width, int height,
            int nrows, int row_base, int block_rows, int block_stride, uint8_t* out, size_t pitch,
-           size_t frame_stride, float* dbg_rgba, int32_t* dbg_steps, sr_stream stream) {
+           size_t frame_stride, float* dbg_rgba, int32_t* dbg_steps, sr_stream stream,
+           const int* d_block_list = nullptr) {
     if (!ctx) return SR_E_INVALID;
     if (!ctx->scene_set) return SR_E_NOT_READY;
     if (!cams || n_frames < 1) return SR_E_INVALID;
@@ -528,6 +557,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.row_base = row_base;
     fr.block_rows = block_rows;
     fr.block_stride = block_stride;
+    fr.block_list = d_block_list;
     if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
@@ -537,7 +567,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     int* order = nullptr;
     int* cost = nullptr;
     if (nrows > 0) {
-        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, &order, &cost);
+        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, d_block_list, &order, &cost);
         if (rc != SR_OK) return rc;
         ctx->last_order = order;
         ctx->last_slots = (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) +
@@ -620,6 +650,7 @@ void sr_destroy(sr_ctx* c) {
         (void)hipFree(kv.second.order);
         (void)hipFree(kv.second.cost);
     }
+    for (auto& kv : c->block_lists) (void)hipFree(kv.second);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     delete c;
 }
@@ -797,6 +828,22 @@ int sr_render_blocks(sr_ctx* c, const sr_camera* cam, const sr_params* p, int wi
     for (int b = block_first; b * block_rows < height; b += block_step) nblocks++;
     return launch(c, cam, 1, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
                   block_step * block_rows, out, pitch, 0, nullptr, nullptr, stream);
+}
+
+int sr_render_block_list(sr_ctx* c, const sr_camera* cams, int n_frames, const sr_params* p, int width, int height,
+                         int block_rows, const int* blocks, int n_blocks, uint8_t* out, size_t pitch,
+                         size_t frame_stride, sr_stream stream) {
+    if (!c || !out || !blocks || block_rows <= 0 || n_blocks <= 0 || height <= 0) return SR_E_INVALID;
+    if ((long long)n_blocks * block_rows > (1 << 24)) return SR_E_INVALID;
+    const int nb = (height + block_rows - 1) / block_rows;
+    for (int i = 0; i < n_blocks; i++)
+        if (blocks[i] < -1 || blocks[i] >= nb) return SR_E_INVALID;
+    if (!hip_ok(hipSetDevice(c->device))) return SR_E_HIP;
+    const int* d = nullptr;
+    const int rc = ensure_block_list(c, blocks, n_blocks, reinterpret_cast<hipStream_t>(stream), &d);
+    if (rc != SR_OK) return rc;
+    return launch(c, cams, n_frames, p, width, height, n_blocks * block_rows, 0, block_rows, block_rows, out, pitch,
+                  frame_stride, nullptr, nullptr, stream, d);
 }
 
 int sr_render_blocks_batch(sr_ctx* c, const sr_camera* cams, int n_frames, const sr_params* p, int width,

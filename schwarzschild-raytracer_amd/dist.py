@@ -8,6 +8,12 @@ edge rows, so contiguous bands are imbalanced (max/mean 1.14 at 8 ranks);
 interleaving 8-row blocks keeps every rank within a few % of the mean while
 each 8-row block still maps onto whole 8x8 wave tiles.
 
+Cost-balanced lists (balanced_blocks): the same 8-row blocks, assigned from
+a step-count map of the frame (the sum over each block's 8x8 waves of the
+longest ray's steps) so that every rank gets the same number of blocks and
+about the same cost (sr_render_block_list renders a list). Block-cyclic rows
+leave the slowest of 8 ranks 3.6 % above the mean (profiles/r02/s9_*).
+
 Exchange: every rank packs its blocks densely into an equal-size tile
 (padded to the largest share; sr_render_blocks writes exactly that layout)
 and one `gather` brings all tiles to rank 0 into one [world, tile_rows, W, 4]
@@ -40,6 +46,76 @@ def tile_rows(world: int, height: int, block_rows: int) -> int:
     return ((nblocks(height, block_rows) + world - 1) // world) * block_rows
 
 
+def wave_costs(steps, block_rows: int = 8, wave: int = 8):
+    """Per-block cost from a [H, W] map of executed steps: the sum over the
+    block's wave tiles (block_rows x wave pixels) of their longest ray's steps
+    (a wave runs until its last lane is done). numpy or torch -> numpy float64."""
+    s = steps.cpu().numpy() if hasattr(steps, "cpu") else np.asarray(steps)
+    H, W = s.shape
+    hb, wb = nblocks(H, block_rows), (W + wave - 1) // wave
+    pad = np.zeros((hb * block_rows, wb * wave), dtype=np.int64)
+    pad[:H, :W] = s
+    return pad.reshape(hb, block_rows, wb, wave).max(axis=(1, 3)).sum(axis=1).astype(np.float64)
+
+
+def balanced_blocks(costs, world: int) -> list[list[int]]:
+    """Equal-length block lists (padded with -1) of about equal total cost:
+    blocks by descending cost, each to the rank with the least cost so far
+    among those with room (ties: lowest rank). Deterministic: every rank
+    computes the same lists from the same cost map."""
+    costs = [float(c) for c in costs]
+    nb = len(costs)
+    per = (nb + world - 1) // world
+    load = [0.0] * world
+    lists: list[list[int]] = [[] for _ in range(world)]
+    for b in sorted(range(nb), key=lambda i: (-costs[i], i)):
+        r = min((k for k in range(world) if len(lists[k]) < per), key=lambda k: (load[k], k))
+        lists[r].append(b)
+        load[r] += costs[b]
+    return [sorted(l) + [-1] * (per - len(l)) for l in lists]
+
+
+def rows_of_list(blocks, height: int, block_rows: int) -> list[int]:
+    rows = []
+    for b in blocks:
+        if b >= 0:
+            rows.extend(range(b * block_rows, min(height, (b + 1) * block_rows)))
+    return rows
+
+
+def assemble_lists(stacked, lists, height: int, block_rows: int):
+    """Gathered tiles of sr_render_block_list ranks -> frames: [world, tile_rows,
+    W, C] -> [height, W, C], or [world, B, tile_rows, W, C] -> [B, height, W, C];
+    frame block b is slot s of rank r where lists[r][s] == b."""
+    world, per = len(lists), len(lists[0])
+    nb = nblocks(height, block_rows)
+    src = np.full(nb, -1, dtype=np.int64)
+    for r, l in enumerate(lists):
+        for s_, b in enumerate(l):
+            if b >= 0:
+                src[b] = r * per + s_
+    assert (src >= 0).all(), "every block of the frame must be on some rank"
+    batched = stacked.ndim == 5
+    rest = tuple(stacked.shape[3 if batched else 2:])
+    if isinstance(stacked, np.ndarray):
+        if batched:
+            v = stacked.reshape((world, stacked.shape[1], per, block_rows) + rest).swapaxes(0, 1)
+            v = v.reshape((stacked.shape[1], world * per, block_rows) + rest)[:, src]
+            return np.ascontiguousarray(v.reshape((stacked.shape[1], nb * block_rows) + rest)[:, :height])
+        v = stacked.reshape((world * per, block_rows) + rest)[src]
+        return np.ascontiguousarray(v.reshape((nb * block_rows,) + rest)[:height])
+    import torch
+
+    idx = torch.as_tensor(src, device=stacked.device)
+    if batched:
+        B = stacked.shape[1]
+        v = stacked.reshape((world, B, per, block_rows) + rest).transpose(0, 1)
+        v = v.reshape((B, world * per, block_rows) + rest).index_select(1, idx)
+        return v.reshape((B, nb * block_rows) + rest)[:, :height]
+    v = stacked.reshape((world * per, block_rows) + rest).index_select(0, idx)
+    return v.reshape((nb * block_rows,) + rest)[:height]
+
+
 def assemble(stacked, world: int, height: int, block_rows: int):
     """[world, tile_rows, W, C] gathered tiles (rank order) -> [height, W, C]
     frame. numpy arrays or torch tensors. Batched tiles [world, B, tile_rows,
@@ -69,8 +145,9 @@ class FrameGather:
     of [B, tile_rows, W, C] holds B frames (a batched launch); __call__(n)
     gathers the first n of them and returns the [n, H, W, C] frames."""
 
-    def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None):
+    def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None, lists=None):
         self.world, self.rank, self.height, self.block_rows, self.group = world, rank, height, block_rows, group
+        self.lists = lists  # balanced_blocks lists (sr_render_block_list tiles), else block-cyclic
         self.tile = tile
         self.stacked = None
         self.views = None
@@ -94,4 +171,6 @@ class FrameGather:
             return None
         if not assemble_frame:
             return stacked
+        if self.lists is not None:
+            return assemble_lists(stacked, self.lists, self.height, self.block_rows)
         return assemble(stacked, self.world, self.height, self.block_rows)

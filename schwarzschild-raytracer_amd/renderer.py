@@ -131,6 +131,27 @@ class Renderer:
         )
         return out, rows
 
+    def render_block_list(self, cams, params: abi.Params, width: int, height: int, block_rows: int, blocks,
+                          out=None, stream=None):
+        """Rows of an explicit block list (sr_render_block_list; -1 = padding)
+        for len(cams) frames in one launch -> [B, len(blocks) * block_rows, W, 4]."""
+        blocks = [int(b) for b in blocks]
+        B = len(cams)
+        arr = (abi.Camera * B)(*cams)
+        lst = (C.c_int * len(blocks))(*blocks)
+        rows = len(blocks) * block_rows
+        if out is None:
+            out = self.torch.empty((B, rows, width, 4), dtype=self.torch.uint8, device=self.tdev)
+        assert out.is_contiguous() and out.dtype == self.torch.uint8 and tuple(out.shape[:1]) == (B,)
+        assert out[0].numel() >= rows * width * 4
+        abi.check(
+            self.lib.sr_render_block_list(self.ctx, arr, B, C.byref(params), width, height, block_rows, lst,
+                                          len(blocks), C.c_void_p(out.data_ptr()), width * 4, out[0].numel(),
+                                          self._stream(stream)),
+            "sr_render_block_list",
+        )
+        return out
+
     def render_debug(self, cam: abi.Camera, params: abi.Params, width: int, height: int, row_begin: int = 0,
                      row_end: int | None = None, stream=None):
         """(float RGBA FragColor, RGBA8, executed steps) for rows [row_begin, row_end)."""

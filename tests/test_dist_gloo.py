@@ -154,3 +154,115 @@ def test_assemble_batched_matches_per_frame(pkg):
     per = np.stack([D.assemble(stacked[:, b], world, h, 8) for b in range(B)])
     assert np.array_equal(D.assemble(stacked, world, h, 8), per)
     assert np.array_equal(D.assemble(torch.from_numpy(stacked), world, h, 8).numpy(), per)
+
+
+def ring_steps(h, w, seed=0):
+    """A step map shaped like the headline's: a band of long rays (the photon
+    ring) across the middle rows over a noisy background."""
+    rng = np.random.default_rng(seed)
+    s = rng.integers(50, 400, (h, w))
+    yy, xx = np.mgrid[0:h, 0:w]
+    r = np.hypot(yy - h * 0.55, (xx - w / 2) * 0.6)
+    s[np.abs(r - h * 0.2) < 6] += 1500
+    return s
+
+
+def test_balanced_blocks_partition_and_balance(pkg):
+    """dist.balanced_blocks: every block exactly once, equal-length lists
+    (padded with -1, the tile height of the block-cyclic split), and a
+    max/mean cost no worse than block-cyclic rows on a ring-shaped map."""
+    D = pkg.dist
+    for h, world in ((1080, 8), (1080, 3), (360, 2), (2160, 8), (37, 4)):
+        steps = ring_steps(h, 96)
+        costs = D.wave_costs(steps, 8)
+        assert len(costs) == D.nblocks(h, 8)
+        lists = D.balanced_blocks(costs, world)
+        assert len(lists) == world and len({len(l) for l in lists}) == 1
+        assert len(lists[0]) * 8 == D.tile_rows(world, h, 8)
+        assert sorted(b for l in lists for b in l if b >= 0) == list(range(D.nblocks(h, 8)))
+        rows = sorted(r for l in lists for r in D.rows_of_list(l, h, 8))
+        assert rows == list(range(h))
+        load = [sum(costs[b] for b in l if b >= 0) for l in lists]
+        cyc = [sum(costs[b] for b in D.blocks_of(k, world, h, 8)) for k in range(world)]
+        assert max(load) / np.mean(load) <= max(cyc) / np.mean(cyc) + 1e-9
+        assert D.balanced_blocks(costs, world) == lists  # deterministic
+
+
+def test_wave_costs_take_each_waves_longest_ray(pkg):
+    D = pkg.dist
+    s = np.zeros((16, 16), dtype=np.int32)
+    s[3, 5] = 7      # block 0, wave 0
+    s[4, 12] = 2     # block 0, wave 1
+    s[9, 1] = 4      # block 1, wave 0
+    s[15, 1] = 9     # block 1, wave 0 (the max)
+    assert D.wave_costs(s, 8).tolist() == [9.0, 9.0]
+    assert D.wave_costs(torch.from_numpy(s), 8).tolist() == [9.0, 9.0]
+
+
+def test_assemble_lists_matches_frame(pkg):
+    D = pkg.dist
+    rng = np.random.default_rng(3)
+    for h, world, B in ((61, 4, 3), (1080, 8, 2), (37, 3, 1)):
+        lists = D.balanced_blocks(D.wave_costs(ring_steps(h, 24, 1), 8), world)
+        frames = rng.integers(0, 255, (B, h, 5, 4)).astype(np.uint8)
+        tr = len(lists[0]) * 8
+        stacked = np.zeros((world, B, tr, 5, 4), dtype=np.uint8)
+        for r, l in enumerate(lists):
+            for s_, b in enumerate(l):
+                if b >= 0:
+                    rows = frames[:, b * 8:(b + 1) * 8]
+                    stacked[r, :, s_ * 8:s_ * 8 + rows.shape[1]] = rows
+        assert np.array_equal(D.assemble_lists(stacked, lists, h, 8), frames)
+        assert np.array_equal(D.assemble_lists(stacked[:, 0], lists, h, 8), frames[0])
+        assert np.array_equal(D.assemble_lists(torch.from_numpy(stacked), lists, h, 8).numpy(), frames)
+        assert np.array_equal(D.assemble_lists(torch.from_numpy(stacked[:, 0].copy()), lists, h, 8).numpy(), frames[0])
+
+
+def list_worker(rank, world, port, q):
+    """sr_render_block_list's layout: rank r's tile slot s holds frame block
+    lists[r][s] (rows of -1 entries stay unwritten); FrameGather(lists=...)
+    reassembles the batched frames on rank 0."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import srpkg
+
+    D = srpkg.load_package().dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        B, h = 4, 93
+        lists = D.balanced_blocks(D.wave_costs(ring_steps(h, 32, 2), 8), world)
+        tile = torch.full((B, len(lists[0]) * 8, 3, 2), -1, dtype=torch.int32)
+        for b in range(B):
+            for k, y in enumerate(D.rows_of_list(lists[rank], h, 8)):
+                tile[b, k, :, 0] = b
+                tile[b, k, :, 1] = y
+        g = D.FrameGather(tile, world, rank, h, 8, lists=lists)
+        frames = g(3)
+        if rank == 0:
+            q.put(frames.numpy().copy())
+        else:
+            assert frames is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_balanced_list_gather_reassembles_frames(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=list_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    frames = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    assert frames.shape == (3, 93, 3, 2)
+    for b in range(3):
+        assert (frames[b, :, :, 0] == b).all()
+        assert frames[b, :, 0, 1].tolist() == list(range(93))

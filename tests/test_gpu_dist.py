@@ -3,7 +3,8 @@ ranks sharing the one leased GPU (gloo backend, tiles staged through host
 memory), three frames in flight, a flyby camera (every frame different).
 Every gathered frame must equal, byte for byte, the frame the single-rank
 run of the same command renders. This executes the distributed init, the
-block-cyclic sr_render_blocks shares, FrameGather, the in-flight pipeline and
+cost-balanced sr_render_block_list shares (and the block-cyclic
+sr_render_blocks_batch ones), FrameGather, the in-flight pipeline and
 the max-over-ranks timing of bench.py (the 8-GPU run uses the same code with
 the nccl backend). Both runs are child processes: this test process never
 touches the GPU."""
@@ -39,8 +40,8 @@ def run(cmd, out):
     return json.loads(line)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world):
+@pytest.mark.parametrize("world,balance", [(2, "cost"), (3, "cost"), (2, "cyclic")])
+def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
     try:
         import torch
     except ImportError:
@@ -48,8 +49,13 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world):
     single = run([sys.executable, "bench.py", "--gpus", "1"], tmp_path / "one")
     multi = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
                  "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(world),
-                 "--dist-backend", "gloo"], tmp_path / "multi")
+                 "--dist-backend", "gloo", "--balance", balance], tmp_path / "multi")
     assert multi["n_gpus"] == world and single["n_gpus"] == 1
+    bal = multi["config"]["balance"]
+    if balance == "cost":
+        assert bal["max_over_mean"] <= bal["cyclic_max_over_mean"] + 1e-9, bal
+    else:
+        assert bal is None
     assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["launches_in_flight"] == 3
     one = sorted((tmp_path / "one").glob("frame_*.npy"))
     many = sorted((tmp_path / "multi").glob("frame_*.npy"))

@@ -254,6 +254,39 @@ def test_batch_equals_single_frames(pkg, gpu, split, mode):
             assert np.array_equal(got[f, :rows], ref[f]), (B, first, step, f)
 
 
+def test_block_list_rows_equal_full_frames(pkg, gpu):
+    """sr_render_block_list: an explicit, unordered block list with -1 padding
+    (dist.balanced_blocks' layout) renders, for B flyby frames in one launch,
+    exactly the rows of each whole frame; padding rows stay untouched. Then
+    the lists of every rank reassemble the frames (dist.assemble_lists)."""
+    import torch
+
+    sc, abi, D = pkg.scenes, pkg.abi, pkg.dist
+    gpu.set_scene(sc.scene_default(textured=True))
+    params = abi.default_params(max_steps=1500, percent_black=-1.0)
+    W, H, B = 320, 180, 3
+    cams = [abi.camera_flyby((f + 0.5) / B, 30.0, 10.0) for f in range(B)]
+    full = [gpu.render(c, params, W, H).cpu().numpy() for c in cams]
+    _, _, steps = gpu.render_debug(cams[0], params, W, H)
+    torch.cuda.synchronize()
+    blocks = [5, 0, 22, -1, 13, 7, -1]
+    out = torch.full((B, len(blocks) * 8, W, 4), 77, dtype=torch.uint8, device="cuda")
+    for _ in range(2):  # the second launch runs the learned order
+        gpu.render_block_list(cams, params, W, H, 8, blocks, out=out)
+    got = out.cpu().numpy()
+    for f in range(B):
+        for s, b in enumerate(blocks):
+            rows = got[f, s * 8:(s + 1) * 8]
+            n = 0 if b < 0 else min(8, H - b * 8)  # block 22 holds the frame's last 4 rows
+            assert (rows[n:] == 77).all()
+            if n:
+                assert np.array_equal(rows[:n], full[f][b * 8:b * 8 + n]), (f, s, b)
+    world = 3
+    lists = D.balanced_blocks(D.wave_costs(steps, 8), world)
+    tiles = np.stack([gpu.render_block_list(cams, params, W, H, 8, l).cpu().numpy() for l in lists])
+    assert np.array_equal(D.assemble_lists(tiles, lists, H, 8), np.stack(full))
+
+
 def test_rows_and_blocks_assemble_full_frame(pkg, gpu):
     import torch
 

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--lib", default="", help="libsr variant to load (default: the package's)")
     ap.add_argument("--batch", type=int, nargs="+", default=[1], help="frames per launch (sr_render_blocks_batch)")
+    ap.add_argument("--balance", choices=["cyclic", "cost"], default="cyclic",
+                    help="rank shares: block-cyclic rows, or dist.balanced_blocks lists (sr_render_block_list)")
     args = ap.parse_args()
     if args.lib:
         os.environ["SR_LIB"] = str(Path(args.lib).resolve())
@@ -59,14 +61,24 @@ def main():
     ss = [torch.cuda.Stream() for _ in range(Fmax)]
     lines = []
     refs = {}
+    lists_of = {}
+    if args.balance == "cost":
+        _, _, steps = rs[0].render_debug(cams[0], params, W, H)
+        costs = D.wave_costs(steps, 8)
+        for _, world in (args.shard or [[0, 1]]):
+            lists_of[world] = D.balanced_blocks(costs, world)
     for (rank, world), Bt, spec in [(sh, b, sp) for sh in (args.shard or [[0, 1]]) for b in args.batch
                                     for sp in args.split]:
         outs = [torch.empty((Bt, D.tile_rows(world, H, 8), W, 4), dtype=torch.uint8, device="cuda")
                 for _ in range(Fmax)]
+        lst = lists_of[world][rank] if world in lists_of else None
 
         def go(k, f, n=None):  # launch f: frames f*Bt .. f*Bt + n - 1 (n <= Bt) on context k
             n = Bt if n is None else n
-            if n == 1:
+            if lst is not None:
+                cs = [cams[(f * Bt + j) % nf] for j in range(n)]
+                rs[k].render_block_list(cs, params, W, H, 8, lst, out=outs[k][:n], stream=ss[k])
+            elif n == 1:
                 rs[k].render_blocks(cams[f * Bt % nf], params, W, H, 8, rank, world, out=outs[k][0], stream=ss[k])
             else:
                 cs = [cams[(f * Bt + j) % nf] for j in range(n)]
@@ -92,6 +104,7 @@ def main():
             torch.cuda.synchronize()
             lat.append(e0.elapsed_time(e1))
         rec = {"lib": Path(args.lib).name if args.lib else "libsr.so", "batch": Bt, "split": spec,
+               "balance": args.balance,
                "shard": f"{rank}/{world}", "camera": args.camera, "latency_ms": round(sorted(lat)[2], 4),
                "identical": same}
         for F in args.inflight:
