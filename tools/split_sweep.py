@@ -69,7 +69,8 @@ def main():
             lists_of[world] = D.balanced_blocks(costs, world)
     for (rank, world), Bt, spec in [(sh, b, sp) for sh in (args.shard or [[0, 1]]) for b in args.batch
                                     for sp in args.split]:
-        outs = [torch.empty((Bt, D.tile_rows(world, H, 8), W, 4), dtype=torch.uint8, device="cuda")
+        # zeroed: padding rows (a share shorter than the tile, -1 list entries) are never written
+        outs = [torch.zeros((Bt, D.tile_rows(world, H, 8), W, 4), dtype=torch.uint8, device="cuda")
                 for _ in range(Fmax)]
         lst = lists_of[world][rank] if world in lists_of else None
 
