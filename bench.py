@@ -299,8 +299,9 @@ def main():
     torch.cuda.synchronize(dev)
     balance = None
     if distributed and args.balance == "cost":
-        # every rank derives the same lists from the same (bit-exact) step map
-        costs = D.wave_costs(steps_full, BLOCK_ROWS)
+        # every rank derives the same lists from the same (bit-exact) per-wave
+        # steps and budget events of the first frame
+        costs = D.block_costs(r.wave_costs(cams[0], params, W, H, stream=stream))
         lists[0] = D.balanced_blocks(costs, world)
         for c in ctxs:
             c[2].lists = lists[0]
@@ -455,8 +456,8 @@ def main():
                 "camera": args.camera,
                 "textures": "assets" if use_assets else "standin",
                 "skybox": quality,
-                "tiling": ((f"cost-balanced {BLOCK_ROWS}-row blocks over {world} ranks (wave-cost map of the first "
-                            "frame), " if balance else f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), ")
+                "tiling": ((f"cost-balanced {BLOCK_ROWS}-row blocks over {world} ranks (per-wave steps and events of "
+                            "the first frame), " if balance else f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), ")
                            + ("RCCL gather to rank 0" if not gloo else "gloo gather of host-staged tiles to rank 0")),
                 "balance": balance,
                 "dist_backend": args.dist_backend if distributed else None,

@@ -306,6 +306,16 @@ int sr_render_block_list(sr_ctx* ctx, const sr_camera* cams, int n_frames, const
                          int height, int block_rows, const int* blocks, int n_blocks, uint8_t* dev_rgba8,
                          size_t pitch_bytes, size_t frame_stride_bytes, sr_stream stream);
 
+/* Per-wave cost map of one whole frame (not in the reference), for
+ * cost-balanced multi-GPU shares: renders the frame (no image output, split
+ * tiles off for this launch) and writes, for each 8x8 wave tile (row block
+ * b = y / 8, column c = x / 8), dev_out[(b * ceil(width / 8) + c) * 2] = the
+ * wave's longest ray's executed steps and [... + 1] = its budget events
+ * (DESIGN.md §5): int32 [ceil(height / 8)][ceil(width / 8)][2]. Deterministic,
+ * so every rank of a node derives the same block lists from it. */
+int sr_wave_costs(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width, int height,
+                  int32_t* dev_out, sr_stream stream);
+
 /* Debug/parity variant: unclamped FragColor as float RGBA (dev_rgba32, may be
  * NULL), the RGBA8 pixel (dev_rgba8, may be NULL) and the number of executed
  * geodesic steps per pixel (dev_steps, may be NULL). Dense rows. */

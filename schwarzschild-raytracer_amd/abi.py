@@ -190,6 +190,7 @@ SIGNATURES = {
     "sr_write_png": (_i, [C.c_char_p, _p, _i, _i, C.c_size_t, _i]),
     "sr_render_blocks_batch": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, _i, _i, _p,
                                     C.c_size_t, C.c_size_t, _p]),
+    "sr_wave_costs": (_i, [_p, C.POINTER(Camera), C.POINTER(Params), _i, _i, _p, _p]),
     "sr_render_block_list": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, C.POINTER(_i), _i, _p,
                                   C.c_size_t, C.c_size_t, _p]),
     "sr_abi_struct_sizes": (_i, [C.POINTER(C.c_size_t), _i]),

@@ -166,6 +166,9 @@ typedef struct {
     // or, when block_list is set (sr_render_block_list): output row k renders
     //   y = block_list[k / block_rows] * block_rows + (k % block_rows), none for -1
     const int32_t* block_list;
+    // optional (sr_wave_costs): per 8x8 wave of the frame, {max steps, budget
+    // events} at [(f * ceil(nrows / 8) + k / 8) * ceil(width / 8) + x / 8]
+    int32_t* wave_cost;
     // textures (RGBA8 texels)
     int32_t bg_w, bg_h;
     int32_t arr_w, arr_h, arr_layers;

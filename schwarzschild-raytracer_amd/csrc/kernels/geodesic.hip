@@ -1485,7 +1485,10 @@ __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, f
 // opaque-classified hit (ST_HIT, logged last) or when the log is full
 // (ST_MORE). Otherwise (resume): stops at the first hit not skipped (ST_HIT,
 // in `hit`). r.i = the stopping step. Ends of the ray: ST_FLAT / ST_BG.
-template <bool CULL, bool RECORD>
+// sr_wave_costs: budget events of each wave of the integrate kernel's workgroup
+__shared__ int sr_lds_ev[SR_WG / 64];
+
+template <bool CULL, bool RECORD, bool WCOST = false>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
@@ -1710,6 +1713,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #ifdef SR_STATS
                 r.ev++;
 #endif
+                // sr_wave_costs: the wave's event count (one lane, its own LDS word)
+                if (WCOST && (int)__lane_id() == __builtin_ctzll(__ballot(1)))
+                    sr_lds_ev[threadIdx.x >> 6] += 1;
                 // a new frame (reseed): the cylinders' direction tests start over
                 SR_PT(2);
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead);
@@ -1821,7 +1827,9 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // part `part` (SR_WG threads) of launch code order[slot] of frame f of the
 // batch (costliest tiles of every frame first, sr_order_kernel), and records
 // the tile's cost (max steps of its rays over the batch).
-template <bool CULL>
+// WCOST: the sr_wave_costs instantiation (per-wave steps and events to
+// fr.wave_cost); the frame kernels carry none of its code.
+template <bool CULL, bool WCOST = false>
 __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
@@ -1861,6 +1869,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
     if ((threadIdx.x & 63) < SR_PROF_N) prof_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
     const unsigned long long prof_t0 = clock64();
 #endif
+    if (WCOST && (threadIdx.x & 63) == 0) sr_lds_ev[threadIdx.x >> 6] = 0;
     if (tid >= 0 && pixel_of(fr, block, tid, q)) {
         const size_t id = ((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256 + tid;
         Tex tx;
@@ -1878,7 +1887,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
-        if (st < 0) st = integrate<CULL, true>(sc, segs, tbl, fr, tx, r, hit, log);
+        if (st < 0) st = integrate<CULL, true, WCOST>(sc, segs, tbl, fr, tx, r, hit, log);
         ps.puti(PS_STATUS, id, st);
         ps.puti(PS_STEPS, id, r.steps);
         ps.puti(PS_NHITS, id, log.n);
@@ -1940,6 +1949,20 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
         if ((threadIdx.x & 63) == 0) atomicMax(&cost[block], steps);
+    }
+    if (WCOST && !(code & SR_SPLIT)) {  // sr_wave_costs (split tiles off)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+        if ((threadIdx.x & 63) == 0) {
+            const int wave = ttid >> 6, gxt = (fr.width + 15) >> 4;
+            const int b8 = (block / gxt) * 2 + (wave >> 1), c8 = (block % gxt) * 2 + (wave & 1);
+            const int nb8 = (fr.nrows + 7) >> 3, nc8 = (fr.width + 7) >> 3;
+            if (b8 < nb8 && c8 < nc8) {
+                int* o = fr.wave_cost + (((size_t)frame * nb8 + b8) * nc8 + c8) * 2;
+                o[0] = steps;
+                o[1] = sr_lds_ev[threadIdx.x >> 6];
+            }
+        }
     }
 }
 
@@ -2117,7 +2140,10 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
-    if (cull)
+    if (fr->wave_cost)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
+                           sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (cull)
         hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
                            tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else

@@ -538,7 +538,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
 int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* params, int width, int height,
            int nrows, int row_base, int block_rows, int block_stride, uint8_t* out, size_t pitch,
            size_t frame_stride, float* dbg_rgba, int32_t* dbg_steps, sr_stream stream,
-           const int* d_block_list = nullptr) {
+           const int* d_block_list = nullptr, int32_t* d_wave_cost = nullptr) {
     if (!ctx) return SR_E_INVALID;
     if (!ctx->scene_set) return SR_E_NOT_READY;
     if (!cams || n_frames < 1) return SR_E_INVALID;
@@ -558,6 +558,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.block_rows = block_rows;
     fr.block_stride = block_stride;
     fr.block_list = d_block_list;
+    fr.wave_cost = d_wave_cost;
     if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
@@ -828,6 +829,18 @@ int sr_render_blocks(sr_ctx* c, const sr_camera* cam, const sr_params* p, int wi
     for (int b = block_first; b * block_rows < height; b += block_step) nblocks++;
     return launch(c, cam, 1, p, width, height, nblocks * block_rows, block_first * block_rows, block_rows,
                   block_step * block_rows, out, pitch, 0, nullptr, nullptr, stream);
+}
+
+int sr_wave_costs(sr_ctx* c, const sr_camera* cam, const sr_params* p, int width, int height, int32_t* dev_out,
+                  sr_stream stream) {
+    if (!c || !cam || !dev_out || width <= 0 || height <= 0) return SR_E_INVALID;
+    // split tiles off for this launch: every wave is a whole 8x8 wave tile
+    const int split = c->split_tiles;
+    c->split_tiles = 0;
+    const int rc = launch(c, cam, 1, p, width, height, height, 0, height, height, nullptr, (size_t)width * 4, 0,
+                          nullptr, nullptr, stream, nullptr, dev_out);
+    c->split_tiles = split;
+    return rc;
 }
 
 int sr_render_block_list(sr_ctx* c, const sr_camera* cams, int n_frames, const sr_params* p, int width, int height,

@@ -9,10 +9,12 @@ interleaving 8-row blocks keeps every rank within a few % of the mean while
 each 8-row block still maps onto whole 8x8 wave tiles.
 
 Cost-balanced lists (balanced_blocks): the same 8-row blocks, assigned from
-a step-count map of the frame (the sum over each block's 8x8 waves of the
-longest ray's steps) so that every rank gets the same number of blocks and
-about the same cost (sr_render_block_list renders a list). Block-cyclic rows
-leave the slowest of 8 ranks 3.6 % above the mean (profiles/r02/s9_*).
+a per-wave cost map of the frame (sr_wave_costs: each 8x8 wave's longest
+ray's steps and its budget events; block_costs) so that every rank gets the
+same number of blocks and about the same cost (sr_render_block_list renders
+a list). Block-cyclic rows leave the slowest of 8 ranks 3.6 % above the mean
+(profiles/r02/s9_*); balancing on steps alone missed the events (a share's
+time fits steps + ~8 x events, profiles/r02/s15_*).
 
 Exchange: every rank packs its blocks densely into an equal-size tile
 (padded to the largest share; sr_render_blocks writes exactly that layout)
@@ -58,21 +60,62 @@ def wave_costs(steps, block_rows: int = 8, wave: int = 8):
     return pad.reshape(hb, block_rows, wb, wave).max(axis=(1, 3)).sum(axis=1).astype(np.float64)
 
 
+EVENT_STEPS = 8.0  # one budget event costs about as much as this many wave steps (profiles/r02/s15_*)
+
+
+def block_costs(wave_cost, event_steps: float = EVENT_STEPS):
+    """Per 8-row block cost from sr_wave_costs' [rows / 8, cols / 8, 2] map:
+    the sum over the block's waves of steps + event_steps x events."""
+    w = wave_cost.cpu().numpy() if hasattr(wave_cost, "cpu") else np.asarray(wave_cost)
+    w = w.astype(np.float64)
+    return (w[..., 0] + event_steps * w[..., 1]).sum(axis=1)
+
+
 def balanced_blocks(costs, world: int) -> list[list[int]]:
     """Equal-length block lists (padded with -1) of about equal total cost:
     blocks by descending cost, each to the rank with the least cost so far
-    among those with room (ties: lowest rank). Deterministic: every rank
-    computes the same lists from the same cost map."""
+    among those with room (ties: lowest rank), then pairwise swaps (a pad
+    counts as a block of cost 0) that lower the most loaded rank's cost. The
+    block-cyclic lists are returned instead when they are at least as even.
+    Deterministic: every rank computes the same lists from the same costs."""
     costs = [float(c) for c in costs]
     nb = len(costs)
     per = (nb + world - 1) // world
+    cost = lambda b: costs[b] if b >= 0 else 0.0  # noqa: E731
     load = [0.0] * world
     lists: list[list[int]] = [[] for _ in range(world)]
     for b in sorted(range(nb), key=lambda i: (-costs[i], i)):
         r = min((k for k in range(world) if len(lists[k]) < per), key=lambda k: (load[k], k))
         lists[r].append(b)
         load[r] += costs[b]
-    return [sorted(l) + [-1] * (per - len(l)) for l in lists]
+    for l in lists:
+        l.extend([-1] * (per - len(l)))
+    for _ in range(4 * nb):  # swaps out of the most loaded rank while one lowers the pair's maximum
+        hi = max(range(world), key=lambda k: (load[k], -k))
+        best = None
+        for r in range(world):
+            if r == hi:
+                continue
+            for i, a in enumerate(lists[hi]):
+                for j, b in enumerate(lists[r]):
+                    d = cost(a) - cost(b)
+                    if d <= 0:
+                        continue
+                    m = max(load[hi] - d, load[r] + d)
+                    if m < load[hi] - 1e-9 and (best is None or m < best[0]):
+                        best = (m, r, i, j, d)
+        if best is None:
+            break
+        _, r, i, j, d = best
+        lists[hi][i], lists[r][j] = lists[r][j], lists[hi][i]
+        load[hi] -= d
+        load[r] += d
+    cyc = [[b for b in range(k, nb, world)] for k in range(world)]
+    cyc = [l + [-1] * (per - len(l)) for l in cyc]
+    cyc_max = max(sum(cost(b) for b in l) for l in cyc)
+    if cyc_max <= max(load):
+        return cyc
+    return [sorted(b for b in l if b >= 0) + [-1] * l.count(-1) for l in lists]
 
 
 def rows_of_list(blocks, height: int, block_rows: int) -> list[int]:

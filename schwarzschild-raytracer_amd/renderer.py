@@ -131,6 +131,14 @@ class Renderer:
         )
         return out, rows
 
+    def wave_costs(self, cam: abi.Camera, params: abi.Params, width: int, height: int, stream=None):
+        """sr_wave_costs: int32 [ceil(H / 8), ceil(W / 8), 2] per 8x8 wave tile of
+        the frame: {longest ray's steps, budget events}. Asynchronous."""
+        out = self.torch.zeros(((height + 7) // 8, (width + 7) // 8, 2), dtype=self.torch.int32, device=self.tdev)
+        abi.check(self.lib.sr_wave_costs(self.ctx, C.byref(cam), C.byref(params), width, height,
+                                         C.c_void_p(out.data_ptr()), self._stream(stream)), "sr_wave_costs")
+        return out
+
     def render_block_list(self, cams, params: abi.Params, width: int, height: int, block_rows: int, blocks,
                           out=None, stream=None):
         """Rows of an explicit block list (sr_render_block_list; -1 = padding)

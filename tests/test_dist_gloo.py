@@ -266,3 +266,16 @@ def test_balanced_list_gather_reassembles_frames(world):
     for b in range(3):
         assert (frames[b, :, :, 0] == b).all()
         assert frames[b, :, 0, 1].tolist() == list(range(93))
+
+
+def test_block_costs_weigh_events(pkg):
+    """dist.block_costs: per 8-row block, the sum over its waves of steps +
+    EVENT_STEPS x events (sr_wave_costs' layout [rows / 8, cols / 8, 2])."""
+    D = pkg.dist
+    w = np.zeros((3, 4, 2), dtype=np.int32)
+    w[0, :, 0] = 100
+    w[1, 2] = (50, 10)
+    w[2, 0] = (0, 0)
+    c = D.block_costs(w)
+    assert c.tolist() == [400.0, 50.0 + D.EVENT_STEPS * 10, 0.0]
+    assert D.block_costs(torch.from_numpy(w), event_steps=0.0).tolist() == [400.0, 50.0, 0.0]

@@ -287,6 +287,46 @@ def test_block_list_rows_equal_full_frames(pkg, gpu):
     assert np.array_equal(D.assemble_lists(tiles, lists, H, 8), np.stack(full))
 
 
+def test_wave_costs_map(pkg, gpu):
+    """sr_wave_costs: per 8x8 wave, the longest ray's steps (the integrate
+    kernel's count: at least render_debug's, which stops at the first hit the
+    shade kernel finds opaque where the step loop logged it as possibly
+    translucent and ran on) and the wave's budget events; deterministic, and the
+    context's split setting is left as it was. dist.block_costs and
+    balanced_blocks turn it into the ranks' lists."""
+    import torch
+
+    sc, abi, D = pkg.scenes, pkg.abi, pkg.dist
+    gpu.set_scene(sc.scene_default(textured=True))
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+    W, H = 328, 184  # partial wave columns at the right edge
+    cam = abi.default_camera()
+    gpu.set_split(16, 4, 1)
+    a = gpu.wave_costs(cam, params, W, H).cpu().numpy()
+    b = gpu.wave_costs(cam, params, W, H).cpu().numpy()
+    assert np.array_equal(a, b)
+    _, _, steps = gpu.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    s = steps.cpu().numpy()
+    assert a.shape == ((H + 7) // 8, (W + 7) // 8, 2)
+    pad = np.zeros((a.shape[0] * 8, a.shape[1] * 8), dtype=np.int64)
+    pad[:H, :W] = s
+    mx = pad.reshape(a.shape[0], 8, a.shape[1], 8).max(axis=(1, 3))
+    assert (a[..., 0] >= mx).all() and (a[..., 0] == mx).mean() > 0.95
+    assert (a[..., 1] >= 0).all() and a[..., 1].sum() > 0
+    assert (a[..., 1][a[..., 0] == 0] == 0).all()
+    costs = D.block_costs(a)
+    assert costs.shape == (a.shape[0],) and (costs > 0).all()
+    lists = D.balanced_blocks(costs, 4)
+    assert sorted(x for l in lists for x in l if x >= 0) == list(range(a.shape[0]))
+    # the split setting survives: a split render still equals the plain frame
+    ref = gpu.render(cam, params, W, H).cpu().numpy()
+    for _ in range(2):
+        out = gpu.render(cam, params, W, H).cpu().numpy()
+    assert np.array_equal(out, ref)
+    gpu.set_split(0)
+
+
 def test_rows_and_blocks_assemble_full_frame(pkg, gpu):
     import torch
 

@@ -63,8 +63,7 @@ def main():
     refs = {}
     lists_of = {}
     if args.balance == "cost":
-        _, _, steps = rs[0].render_debug(cams[0], params, W, H)
-        costs = D.wave_costs(steps, 8)
+        costs = D.block_costs(rs[0].wave_costs(cams[0], params, W, H))
         for _, world in (args.shard or [[0, 1]]):
             lists_of[world] = D.balanced_blocks(costs, world)
     for (rank, world), Bt, spec in [(sh, b, sp) for sh in (args.shard or [[0, 1]]) for b in args.batch
