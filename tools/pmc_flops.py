@@ -9,7 +9,7 @@ profiles/pmc_latest.json for bench.py's roofline.
 Every directory holds one rocprofv3 run (`-d DIR -o run --output-format csv`).
 Counters are summed over XCDs / shader engines per dispatch and averaged over
 the integrate dispatches of the frame's grid (the most common grid size of
-sr_integrate_kernel<true>: bench.py's frames; the step-count and band launches
+sr_integrate_kernel<true, false>: bench.py's frames; the step-count and band launches
 have other grids or are few).
 """
 from __future__ import annotations
@@ -63,7 +63,7 @@ def calib_factors(root):
     return rows
 
 
-def frame_counters(roots, kernel="sr_integrate_kernel<true>"):
+def frame_counters(roots, kernel="sr_integrate_kernel<true, false>"):
     per = collections.defaultdict(list)
     grids = collections.Counter()
     recs = []
@@ -133,7 +133,7 @@ def main():
     flop = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * k_flop  # transcendentals included (1 each)
     trans = c.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0) * k_trans
     rec = {
-        "kernel": "sr_integrate_kernel<true>",
+        "kernel": "sr_integrate_kernel<true, false>",
         "kernel_sha": bench.kernel_sha(),
         "width": args.width,
         "height": args.height,

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """profiles/traffic_latest.json from a FETCH_SIZE / WRITE_SIZE PMC session
 (tools/pmc_session.sh, separate passes) of the headline frame:
-per-launch HBM-side bytes of sr_integrate_kernel<true>.
+per-launch HBM-side bytes of sr_integrate_kernel<true, false>.
 
 rocprofv3 reports both in KiB. MI355X_MICROARCH.md (HBM): FETCH_SIZE reads half
 the bytes of wide (16 B/lane) coalesced streaming reads; this kernel's reads
@@ -35,7 +35,7 @@ def main():
     fetch = c["FETCH_SIZE"] * 1024.0
     write = c["WRITE_SIZE"] * 1024.0
     rec = {
-        "kernel": "sr_integrate_kernel<true>",
+        "kernel": "sr_integrate_kernel<true, false>",
         "kernel_sha": bench.kernel_sha(),
         "width": a.width, "height": a.height, "max_steps": a.max_steps,
         "fetch_bytes_raw": fetch, "fetch_bytes_x2_bound": 2 * fetch, "write_bytes": write,
