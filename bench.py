@@ -304,7 +304,7 @@ def main():
         costs = D.block_costs(r.wave_costs(cams[0], params, W, H, stream=stream))
         lists[0] = D.balanced_blocks(costs, world)
         for c in ctxs:
-            c[2].lists = lists[0]
+            c[2].set_lists(lists[0])
         loads = [sum(costs[b] for b in l if b >= 0) for l in lists[0]]
         cyc = [sum(costs[b] for b in D.blocks_of(k, world, H, BLOCK_ROWS)) for k in range(world)]
         balance = {"max_over_mean": round(max(loads) / (sum(loads) / world), 4),

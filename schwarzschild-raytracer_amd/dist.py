@@ -126,11 +126,9 @@ def rows_of_list(blocks, height: int, block_rows: int) -> list[int]:
     return rows
 
 
-def assemble_lists(stacked, lists, height: int, block_rows: int):
-    """Gathered tiles of sr_render_block_list ranks -> frames: [world, tile_rows,
-    W, C] -> [height, W, C], or [world, B, tile_rows, W, C] -> [B, height, W, C];
-    frame block b is slot s of rank r where lists[r][s] == b."""
-    world, per = len(lists), len(lists[0])
+def list_sources(lists, height: int, block_rows: int):
+    """Frame block b -> its slot r * per + s in the stacked tiles (lists[r][s] == b)."""
+    per = len(lists[0])
     nb = nblocks(height, block_rows)
     src = np.full(nb, -1, dtype=np.int64)
     for r, l in enumerate(lists):
@@ -138,6 +136,18 @@ def assemble_lists(stacked, lists, height: int, block_rows: int):
             if b >= 0:
                 src[b] = r * per + s_
     assert (src >= 0).all(), "every block of the frame must be on some rank"
+    return src
+
+
+def assemble_lists(stacked, lists, height: int, block_rows: int, src=None):
+    """Gathered tiles of sr_render_block_list ranks -> frames: [world, tile_rows,
+    W, C] -> [height, W, C], or [world, B, tile_rows, W, C] -> [B, height, W, C];
+    frame block b is slot s of rank r where lists[r][s] == b. src: list_sources
+    (for torch, a tensor on the tiles' device: no host copy per call)."""
+    world, per = len(lists), len(lists[0])
+    nb = nblocks(height, block_rows)
+    if src is None:
+        src = list_sources(lists, height, block_rows)
     batched = stacked.ndim == 5
     rest = tuple(stacked.shape[3 if batched else 2:])
     if isinstance(stacked, np.ndarray):
@@ -149,7 +159,7 @@ def assemble_lists(stacked, lists, height: int, block_rows: int):
         return np.ascontiguousarray(v.reshape((nb * block_rows,) + rest)[:height])
     import torch
 
-    idx = torch.as_tensor(src, device=stacked.device)
+    idx = src if isinstance(src, torch.Tensor) else torch.as_tensor(src, device=stacked.device)
     if batched:
         B = stacked.shape[1]
         v = stacked.reshape((world, B, per, block_rows) + rest).transpose(0, 1)
@@ -191,12 +201,23 @@ class FrameGather:
     def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None, lists=None):
         self.world, self.rank, self.height, self.block_rows, self.group = world, rank, height, block_rows, group
         self.lists = lists  # balanced_blocks lists (sr_render_block_list tiles), else block-cyclic
+        self._src = None  # the lists' block sources on the tiles' device (made once)
         self.tile = tile
         self.stacked = None
         self.views = None
         if rank == 0 and world > 1:
             self.stacked = tile.new_empty((world,) + tuple(tile.shape))
             self.views = [self.stacked[i] for i in range(world)]
+
+    def set_lists(self, lists):
+        """Switch to balanced_blocks lists; their block sources go to the tiles'
+        device now, outside any launch."""
+        self.lists = lists
+        self._src = None
+        if hasattr(self.tile, "device"):
+            import torch
+
+            self._src = torch.as_tensor(list_sources(lists, self.height, self.block_rows), device=self.tile.device)
 
     def __call__(self, n: int | None = None, assemble_frame: bool = True):
         import torch.distributed as dist
@@ -215,5 +236,12 @@ class FrameGather:
         if not assemble_frame:
             return stacked
         if self.lists is not None:
-            return assemble_lists(stacked, self.lists, self.height, self.block_rows)
+            if self._src is None or self._src.device != stacked.device:
+                import torch
+
+                # built once: a per-call host-to-device copy of the index would
+                # wait for the launch's stream (the frame's whole render)
+                self._src = torch.as_tensor(list_sources(self.lists, self.height, self.block_rows),
+                                            device=stacked.device)
+            return assemble_lists(stacked, self.lists, self.height, self.block_rows, self._src)
         return assemble(stacked, self.world, self.height, self.block_rows)

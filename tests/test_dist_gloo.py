@@ -242,6 +242,10 @@ def list_worker(rank, world, port, q):
                 tile[b, k, :, 1] = y
         g = D.FrameGather(tile, world, rank, h, 8, lists=lists)
         frames = g(3)
+        g2 = D.FrameGather(tile, world, rank, h, 8)
+        g2.set_lists(lists)
+        frames2 = g2(3)
+        assert (frames is None) == (frames2 is None) and (frames is None or torch.equal(frames, frames2))
         if rank == 0:
             q.put(frames.numpy().copy())
         else:
