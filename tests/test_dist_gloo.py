@@ -283,3 +283,14 @@ def test_block_costs_weigh_events(pkg):
     c = D.block_costs(w)
     assert c.tolist() == [400.0, 50.0 + D.EVENT_STEPS * 10, 0.0]
     assert D.block_costs(torch.from_numpy(w), event_steps=0.0).tolist() == [400.0, 50.0, 0.0]
+
+
+def test_balanced_blocks_edge_cases(pkg):
+    """More ranks than blocks (ranks with only padding), all-zero costs (the
+    block-cyclic lists), and one dominant block (the swaps move the rest)."""
+    D = pkg.dist
+    assert D.balanced_blocks([5.0, 1.0, 3.0], 8) == [[0], [1], [2]] + [[-1]] * 5
+    assert D.balanced_blocks([0.0] * 5, 2) == [[0, 2, 4], [1, 3, -1]]
+    lists = D.balanced_blocks([10.0] + [1.0] * 10, 2)
+    loads = [sum(([10.0] + [1.0] * 10)[b] for b in l if b >= 0) for l in lists]
+    assert sorted(loads) == [6.0, 14.0] and all(len(l) == 6 for l in lists)
