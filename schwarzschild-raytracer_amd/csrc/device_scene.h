@@ -90,7 +90,7 @@ typedef struct {
     float pos[3], x1;
     float a0[3], x2;  // axes[0..2] (columns)
     float a1[3], pad0;
-    float a2[3], pad1;
+    float a2[3], cn;  // cn: |bc| x 1.001, rounded up (outward_clear)
 } sr_dev_slot;  // 128 B
 
 // Per-pixel state planes passed between the integrate / shade / resume kernels
@@ -169,6 +169,9 @@ typedef struct {
     // optional (sr_wave_costs): per 8x8 wave of the frame, {max steps, budget
     // events} at [(f * ceil(nrows / 8) + k / 8) * ceil(width / 8) + x / 8]
     int32_t* wave_cost;
+    // 1 - (max_angle / max_steps)^2 / 8, rounded down: a chord between two
+    // orbit points at radii >= a stays at least a x out_dip from the origin
+    float out_dip;
     // textures (RGBA8 texels)
     int32_t bg_w, bg_h;
     int32_t arr_w, arr_h, arr_layers;

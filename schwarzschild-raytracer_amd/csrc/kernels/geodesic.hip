@@ -406,6 +406,29 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
 __device__ __forceinline__ float clearance_bh(float a) {
     return (fabsf(a - 1.0f) - SR_MU_QUADRATIC * 3.0f) - 1.8f * SR_MU_QUADRATIC * a;
 }
+// Outward lanes: past the photon orbit (u < 0.6) with u' < 0, u'' = -u (1 -
+// 1.5 u) < 0 keeps u falling, so every later orbit point lies farther from
+// the origin than the anchor (distance a), and every later chord stays
+// beyond a x out_dip. Slot j cannot be hit again once that exceeds the
+// farthest reach of its per-chord acceptance region, |c| + br + mu S (plus a
+// cylinder's quadratic margin qk (S + |pos|_1)^2 while no chord of the orbit
+// can be nearly parallel to its axis, bs.cm), for the chords there (S <= 2 a
+// + 1 + 0.01 a^2 covers |o|_1 + len + 1 of an orbit chord at radius up to
+// 110; the bound grows slower than a, so it holds for every later chord
+// too). The black hole's region is the r = 1 shell; planes are unbounded. A
+// new orbital frame (reseed) re-anchors every slot. Escaping rays stop
+// re-anchoring the hole and the objects they have passed: events 686 k ->
+// 552 k per headline frame, -6 % frame time (profiles/r02/s18_*).
+__device__ __forceinline__ bool outward_clear(float cn, float br, float mu, float qk, float pl1, float a, float dip) {
+    const float S = __builtin_fmaf(0.01f * a, a, __builtin_fmaf(2.0f, a, 1.0f));
+    const float Sc = S + pl1;
+    return a * dip > (cn + br + __builtin_fmaf(mu, S, qk * Sc * Sc)) * 1.001f;
+}
+// slot j >= 1 for an outward lane at distance a (cyl_par: bs.cm's bit for a budgeted cylinder)
+__device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par, float a, float dip) {
+    if (sl.type == SR_OBJECT_PLANE || (sl.type == SR_OBJECT_CYLINDER && (cyl_par || !(sl.x1 > 0.0f)))) return false;
+    return outward_clear(sl.cn, sl.br, sl.mu, sl.type == SR_OBJECT_CYLINDER ? sl.qk : 0.0f, sl.pl1, a, dip);
+}
 __device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
     return j == 0 ? clearance_bh(a) : clearance_obj(sc->slots[j - 1], A, a);
 }
@@ -533,14 +556,26 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
     bs.cm = cm;
 }
 
-__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv) {
+// bs.cm's bit for slot j (budgeted cylinders; false for other slots)
+__device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc, const Budget& bs, int j) {
+    const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;
+    if (!((cyl >> (j - 1)) & 1u)) return false;
+    return (bs.cm >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
+}
+
+__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv,
+                                            bool outward, float dip) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
     float m = INFINITY;
+    budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
 #pragma unroll 1
     for (int j = 0; j <= nb; j++) {
-        const float e = clearance(sc, j, A, a);
+        float e = clearance(sc, j, A, a);
+        if (outward && (j == 0 ? outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)
+                               : outward_slot(sc->slots[j - 1], cyl_par_bit(sc, bs, j), a, dip)))
+            e = INFINITY;
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
     }
@@ -557,7 +592,6 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         }
     }
     bs.mh = mh;
-    budget_frame(sc, bs, nv, tv);
 }
 
 // The orbit's (pa, pb) on each budgeted cylinder's axis (budget_frame),
@@ -692,7 +726,8 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // slots some lane has spent - usually one - run their clearance and reach
 // tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
-                                                 float perr, uint32_t par, bool reanchor_cyl, float ahead) {
+                                                 float perr, uint32_t par, bool reanchor_cyl, float ahead,
+                                                 bool outward, float dip) {
     constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -714,6 +749,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             }
         }
     }
+    if (reanchor_cyl) forced |= (2u << nb) - 1u;  // a new orbital frame: outward budgets start over
     uint32_t spent = 0;  // wave-uniform: slots some lane has spent or is about to
     uint32_t hard = forced;  // this lane's slots whose budget does not cover the chord
 #pragma unroll
@@ -771,7 +807,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         // (the others re-anchor early: look-ahead, or another lane spent it)
         const bool h = (hard >> j) & 1u;
         if (j == 0) {
-            const float v = clearance_bh(a) - perr;
+            const float v = (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip))
+                                ? INFINITY
+                                : clearance_bh(a) - perr;
             bs.E[0] = v;
             m = nmin(m, v);
             if (__ballot(h) && __ballot(h && slot_reachable(nullptr, 0, A, B, perr))) reach |= 1u;
@@ -784,7 +822,12 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             constexpr int TY = decltype(ty_tag)::value;
             sr_dev_slot st = sl;
             st.type = TY;
-            const float v = clearance_obj(st, B, a) - perr;
+            float v = clearance_obj(st, B, a) - perr;
+            if (TY != SR_OBJECT_PLANE && outward &&
+                outward_slot(st, TY == SR_OBJECT_CYLINDER &&
+                                     ((bs.cm >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
+                             a, dip))
+                v = INFINITY;
             bs.E[j * SR_E_STRIDE] = v;
             m = nmin(m, v);
             if (TY == SR_OBJECT_CYLINDER) {
@@ -1495,7 +1538,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     __shared__ float lds_E[SR_E_ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     Budget bs;
     bs.E = lds_E + threadIdx.x;
-    if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv);
+    if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -1718,7 +1761,22 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     sr_lds_ev[threadIdx.x >> 6] += 1;
                 // a new frame (reseed): the cylinders' direction tests start over
                 SR_PT(2);
-                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead);
+#ifdef SR_STATS_BH  // measurement only: the black hole's triggering lanes by orbit state
+                {
+                    const bool h0 = !(bs.T < bs.E[0]);
+                    const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
+                    SR_STAT(23, __popcll(__ballot(h0 && r.u > 1.0f)));
+                    SR_STAT(24, __popcll(__ballot(h0 && r.u <= 1.0f && r.u > 0.9f)));
+                    SR_STAT(25, __popcll(__ballot(h0 && ring)));
+                    SR_STAT(26, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && r.du > 0.0f)));
+                    SR_STAT(27, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && !(r.du > 0.0f))));
+                    SR_STAT(28, __popcll(__ballot(event)));
+                    SR_STAT(29, __popcll(__ballot(h0)));
+                    SR_STAT(30, __ballot(h0) != 0ull);
+                    SR_STAT(31, __popcll(__ballot(1)));
+                }
+#endif
+                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);

@@ -527,6 +527,10 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.arr_w = ctx->arr_w;
     fr.arr_h = ctx->arr_h;
     fr.arr_layers = ctx->arr_layers;
+    {
+        const double dphi = (double)fr.max_angle / (p->max_steps > 0 ? p->max_steps : 1);
+        fr.out_dip = (float)(1.0 - dphi * dphi / 8.0 - 1e-6);
+    }
     fr.split_tiles = ctx->split_tiles;
     fr.split_log2 = ctx->split_log2;
     fr.split_min_steps = ctx->split_min_steps;
@@ -696,6 +700,9 @@ static void pack_slot(const sr_dev_obj& o, int cyl, sr_dev_slot& sl) {
     sl.mu = o.mu;
     sl.pl1 = o.pl1;
     std::memcpy(sl.bc, o.bc, sizeof sl.bc);
+    sl.cn = std::nextafter((float)(std::sqrt((double)o.bc[0] * o.bc[0] + (double)o.bc[1] * o.bc[1] +
+                                             (double)o.bc[2] * o.bc[2]) * 1.001),
+                           INFINITY);
     std::memcpy(sl.pos, f + SR_F_POS, 3 * sizeof(float));
     std::memcpy(sl.a0, f + SR_F_AXES, 3 * sizeof(float));
     std::memcpy(sl.a1, f + SR_F_AXES + 3, 3 * sizeof(float));
