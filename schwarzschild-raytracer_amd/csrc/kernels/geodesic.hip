@@ -1776,6 +1776,21 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(1)));
                 }
 #endif
+#ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
+                {
+                    const bool h0 = !(bs.T < bs.E[0]);
+                    const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
+                    SR_STAT(23, __popcll(__ballot(h0 && r.u > 1.0f)));
+                    SR_STAT(24, __popcll(__ballot(h0 && r.u <= 1.0f && r.u > 0.9f)));
+                    SR_STAT(25, __popcll(__ballot(h0 && ring)));
+                    SR_STAT(26, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && r.du > 0.0f)));
+                    SR_STAT(27, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && !(r.du > 0.0f))));
+                    SR_STAT(28, __popcll(__ballot(event)));
+                    SR_STAT(29, __popcll(__ballot(h0)));
+                    SR_STAT(30, __ballot(h0) != 0ull);
+                    SR_STAT(31, __popcll(__ballot(1)));
+                }
+#endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
                 SR_PT(6);
 #ifdef SR_STATS
