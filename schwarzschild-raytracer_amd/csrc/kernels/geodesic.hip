@@ -1815,6 +1815,27 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(1)));
                 }
 #endif
+#ifdef SR_STATS_DIR  // measurement only (tools/stats_dir.py): object triggers by the lane's radial direction
+                {
+                    const bool outw = r.du < 0.0f && r.u < 0.6f;
+                    const bool inc = r.du > 0.0f;
+                    bool any = false;
+#pragma unroll
+                    for (int j = 1; j <= 6; j++) {
+                        const bool h = !(bs.T < bs.E[j * SR_E_STRIDE]);
+                        any |= h;
+                        if (j == 3 || j == 5) {  // the default scene's accretion disk and rectangle
+                            const int b = j == 3 ? 23 : 26;
+                            SR_STAT(b, __popcll(__ballot(h && outw)));
+                            SR_STAT(b + 1, __popcll(__ballot(h && inc)));
+                            SR_STAT(b + 2, __popcll(__ballot(h && !outw && !inc)));
+                        }
+                    }
+                    SR_STAT(29, __popcll(__ballot(any && outw)));
+                    SR_STAT(30, __popcll(__ballot(any && inc)));
+                    SR_STAT(31, __popcll(__ballot(any)));
+                }
+#endif
 #ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
                 {
                     const bool h0 = !(bs.T < bs.E[0]);
