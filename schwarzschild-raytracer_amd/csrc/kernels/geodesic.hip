@@ -786,10 +786,17 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     if (reanchor_cyl) forced |= (2u << nb) - 1u;  // a new orbital frame: outward budgets start over
     uint32_t spent = 0;  // wave-uniform: slots some lane has spent or is about to
     uint32_t hard = forced;  // this lane's slots whose budget does not cover the chord
+    // one ballot per slot of a single compare (written straight to an SGPR
+    // pair); forced slots, rare (reseeds, near-axis chords), balloted apart
 #pragma unroll
     for (int j = 0; j < NS; j++) {
         hard |= (uint32_t)!(T < e[j]) << j;
-        if (__ballot(!(T + ahead < e[j]) || ((forced >> j) & 1u))) spent |= 1u << j;
+        if (__ballot(!(T + ahead < e[j]))) spent |= 1u << j;
+    }
+    if (__ballot(forced != 0u)) {
+#pragma unroll
+        for (int j = 0; j < NS; j++)
+            if (__ballot((forced >> j) & 1u)) spent |= 1u << j;
     }
     spent &= (2u << nb) - 1u;
     SR_PTB(20);
