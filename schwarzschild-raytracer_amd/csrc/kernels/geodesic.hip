@@ -866,7 +866,13 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             float v = clearance_obj(st, B, a) - perr;
             if ((TY == SR_OBJECT_RECTANGLE || TY == SR_OBJECT_DISK || TY == SR_OBJECT_HOLLOW_DISK ||
                  TY == SR_OBJECT_PLANE) && st.mp < INFINITY && v < 0.5f * a) {
-                const float w = plane_window(st, A, B, a, perr);
+                // the window's slot-independent terms (chord length, curvature
+                // bound) recomputed here: hoisted out of the slot loop they
+                // were spilled and reloaded one scratch round trip at a time
+                float ao = a;
+                asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(B.x), "+v"(B.y), "+v"(B.z));
+                asm volatile("" : "+v"(ao), "+v"(perr));
+                const float w = plane_window(st, A, B, ao, perr);
                 v = w > v ? w : v;  // NaN v stays NaN
             }
             if (TY != SR_OBJECT_PLANE && outward &&
