@@ -604,12 +604,17 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     bs.T = 0.0f;
     float m = INFINITY;
     budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
+    {
+        float e = clearance_bh(a);
+        if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
+        bs.E[0] = e;
+        m = nmin(m, e);
+    }
 #pragma unroll 1
-    for (int j = 0; j <= nb; j++) {
-        float e = clearance(sc, j, A, a);
-        if (outward && (j == 0 ? outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)
-                               : outward_slot(sc->slots[j - 1], cyl_par_bit(sc, bs, j), a, dip)))
-            e = INFINITY;
+    for (int j = 1; j <= nb; j++) {
+        const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);  // one batch of scalar loads per slot
+        float e = clearance_obj(sl, A, a);
+        if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
     }
