@@ -463,9 +463,6 @@ __device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par
     if (sl.type == SR_OBJECT_PLANE || (sl.type == SR_OBJECT_CYLINDER && (cyl_par || !(sl.x1 > 0.0f)))) return false;
     return outward_clear(sl.cn, sl.br, sl.mu, sl.type == SR_OBJECT_CYLINDER ? sl.qk : 0.0f, sl.pl1, a, dip);
 }
-__device__ __forceinline__ float clearance(const sr_dev_scene* __restrict__ sc, int j, f3 A, float a) {
-    return j == 0 ? clearance_bh(a) : clearance_obj(sc->slots[j - 1], A, a);
-}
 
 // A budget slot's record read in one batch of scalar loads: every field is
 // pinned to an SGPR where it is loaded, so the type-specific code that
