@@ -503,7 +503,7 @@ __device__ __forceinline__ sr_dev_slot pin_slot(const sr_dev_slot& g) {
 // accepts only a point p = o + lambda d with 0 <= lambda <= len, i.e. on the
 // chord up to rounding, whose computed height passes that window, so this
 // bound holds however ill-conditioned the lateral quadratic is (chords nearly
-// parallel to the axis). Same margins as clearance(); -inf without a unit axis.
+// parallel to the axis). Same margins as clearance_obj(); -inf without a unit axis.
 __device__ __forceinline__ float clearance_slab(const sr_dev_slot& sl, f3 A, float a) {
     if (!(sl.mp < INFINITY)) return -INFINITY;
     const float y = dot(A - ld3(sl.pos), ld3(sl.a1));
