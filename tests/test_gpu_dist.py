@@ -1,5 +1,6 @@
 """The multi-rank bench path on the GPU box: bench.py under torchrun with two
-ranks sharing the one leased GPU (gloo backend, tiles staged through host
+ranks sharing the one leased GPU (and eight, the driver's largest world: padded
+block lists, gloo backend, tiles staged through host
 memory), three frames in flight, a flyby camera (every frame different).
 Every gathered frame must equal, byte for byte, the frame the single-rank
 run of the same command renders. This executes the distributed init, the
@@ -40,7 +41,7 @@ def run(cmd, out):
     return json.loads(line)
 
 
-@pytest.mark.parametrize("world,balance", [(2, "cost"), (3, "cost"), (2, "cyclic")])
+@pytest.mark.parametrize("world,balance", [(2, "cost"), (3, "cost"), (2, "cyclic"), (8, "cost")])
 def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
     try:
         import torch
