@@ -1,7 +1,7 @@
-"""The multi-rank bench path on the GPU box: bench.py under torchrun with two
-ranks sharing the one leased GPU (and eight, the driver's largest world: padded
-block lists, gloo backend, tiles staged through host
-memory), three frames in flight, a flyby camera (every frame different).
+"""The multi-rank bench path on the GPU box: bench.py under torchrun with two,
+three or eight ranks (the driver's largest world: padded block lists) sharing
+the one leased GPU (gloo backend, tiles staged through host memory), three
+frames in flight, a flyby camera (every frame different).
 Every gathered frame must equal, byte for byte, the frame the single-rank
 run of the same command renders. This executes the distributed init, the
 cost-balanced sr_render_block_list shares (and the block-cyclic
