@@ -245,9 +245,13 @@ def main():
 
     frames = {}  # --dump-frames: frame index -> assembled frame (rank 0), timed frames only
     dump_from = [1 << 30]
+    last = [None]  # (first frame, assembled frames) of the last gathered launch, rank 0 (parity check)
 
     def keep(first, batch):
-        if args.dump_frames and batch is not None:
+        if batch is None:
+            return
+        last[0] = (first, batch)
+        if args.dump_frames:
             for i in range(batch.shape[0]):
                 if first + i >= dump_from[0]:
                     frames[first + i] = batch[i].clone()  # on the launch's stream (nccl) or host (gloo)
@@ -265,6 +269,8 @@ def main():
             rk.render_blocks_batch(cams[first:first + n], params, W, H, BLOCK_ROWS, rank, world, out=out[:n],
                                    stream=s_k)
 
+    gtime = {"on": False, "events": [], "host_s": 0.0}  # the timed launches' gathers (N > 1)
+
     def launch(j, first, n):
         rk, tile_k, gather_k, s_k, host_k = ctxs[j % F]
         with torch.cuda.stream(s_k):
@@ -272,13 +278,25 @@ def main():
             if gloo:
                 host_k[:n].copy_(tile_k[:n], non_blocking=True)
                 return
+            if gtime["on"] and distributed:  # HIP events around the RCCL gather on the launch's stream
+                e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                e[0].record(s_k)
+                res = gather_k(n)
+                e[1].record(s_k)
+                gtime["events"].append(e)
+                keep(first, res)
+                return
             keep(first, gather_k(n))  # the assembled frames on rank 0 (RCCL gather for N > 1)
 
     def complete(j, first, n):  # gloo: the launch's host tiles are gathered once its render is done
         if gloo:
             _, _, gather_k, s_k, _ = ctxs[j % F]
             s_k.synchronize()
-            keep(first, gather_k(n))
+            t = time.perf_counter()
+            res = gather_k(n)
+            if gtime["on"]:
+                gtime["host_s"] += time.perf_counter() - t
+            keep(first, res)
 
     def run_frames(first, count):
         """frames first .. first + count - 1 in launches of B (the last takes the rest), F in flight"""
@@ -299,16 +317,22 @@ def main():
     torch.cuda.synchronize(dev)
     balance = None
     if distributed and args.balance == "cost":
-        # every rank derives the same lists from the same (bit-exact) per-wave
-        # steps and budget events of the first frame
-        costs = D.block_costs(r.wave_costs(cams[0], params, W, H, stream=stream))
-        lists[0] = D.balanced_blocks(costs, world)
+        # rank 0 prices the blocks from the first frame's per-wave steps and
+        # budget events and sends every rank the same lists (a rank whose own
+        # cost map differed would otherwise render rows rank 0 does not expect)
+        obj = [None]
+        if rank == 0:
+            costs = D.block_costs(r.wave_costs(cams[0], params, W, H, stream=stream))
+            lst = D.balanced_blocks(costs, world)
+            loads = [sum(costs[b] for b in l if b >= 0) for l in lst]
+            cyc = [sum(costs[b] for b in D.blocks_of(k, world, H, BLOCK_ROWS)) for k in range(world)]
+            obj = [(lst, {"max_over_mean": round(max(loads) / (sum(loads) / world), 4),
+                          "cyclic_max_over_mean": round(max(cyc) / (sum(cyc) / world), 4),
+                          "lists_from": "rank 0 (broadcast)"})]
+        dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
+        lists[0], balance = obj[0]
         for c in ctxs:
             c[2].set_lists(lists[0])
-        loads = [sum(costs[b] for b in l if b >= 0) for l in lists[0]]
-        cyc = [sum(costs[b] for b in D.blocks_of(k, world, H, BLOCK_ROWS)) for k in range(world)]
-        balance = {"max_over_mean": round(max(loads) / (sum(loads) / world), 4),
-                   "cyclic_max_over_mean": round(max(cyc) / (sum(cyc) / world), 4)}
         rows_mine = D.rows_of_list(lists[0][rank], H, BLOCK_ROWS)
     else:
         rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
@@ -334,12 +358,21 @@ def main():
     sync_all()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    gtime["on"] = True
     run_frames(warm, args.steps)
     sync_all()
     torch.cuda.synchronize(dev)
+    t_mine = time.perf_counter() - t0  # this rank's own span, before waiting for the others
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gtime["on"] = False
+    # parity of the last timed frame (rank 0 holds it assembled), before any
+    # further launch reuses its context's tile
+    parity = None
+    if rank == 0 and last[0] is not None:
+        first, batch = last[0]
+        parity = frame_parity(args, W, H, N, quality, use_assets, batch[-1], first + batch.shape[0] - 1)
     ktimes = np.concatenate([c[0].kernel_times(per_ctx) for c in ctxs], axis=0)
     if args.dump_frames and rank == 0:
         Path(args.dump_frames).mkdir(parents=True, exist_ok=True)
@@ -379,10 +412,23 @@ def main():
         speedup_ref = {"culled_ms": round(culled, 4), "reference_loop_ms": round(unculled, 4),
                        "speedup": round(unculled / culled, 2)}
 
+    ranks = None
     if distributed:  # max over ranks (RCCL reduces device tensors, gloo host ones)
         t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=None if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, latency_ms = float(t[0]), float(t[1])
+        # what each rank did, so that an N-GPU line documents itself
+        gms = gtime["host_s"] * 1e3 + sum(a.elapsed_time(b) for a, b in gtime["events"])
+        props = torch.cuda.get_device_properties(dev)
+        mine = {"rank": rank, "world_size": dist.get_world_size(), "local_rank": local, "device": dev.index,
+                "device_name": props.name, "pci_bus_id": getattr(props, "pci_bus_id", None),
+                "visible_devices": os.environ.get("HIP_VISIBLE_DEVICES", os.environ.get("CUDA_VISIBLE_DEVICES")),
+                "rows": len(rows_mine), "share_ms_per_frame": round(t_mine * 1e3 / args.steps, 4),
+                "integrate_kernel_ms": round(float(ktimes[:, 0].mean()), 4),
+                "gather_ms_per_frame": round(gms / args.steps, 4),
+                "gather": "host-staged gloo" if gloo else "RCCL gather, HIP events on the launch streams"}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
 
     ms_per_step = elapsed * 1e3 / args.steps
     mpix_s = W * H * args.steps / elapsed / 1e6
@@ -468,9 +514,12 @@ def main():
                 "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "frame_latency_ms": round(latency_ms, 4),
                 "culling": not args.no_cull,
+                "world_size": world,
+                "ranks": ranks,
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line), flush=True)
     if distributed:
@@ -478,6 +527,46 @@ def main():
         dist.destroy_process_group()
     for c in ctxs:
         c[0].close()
+
+
+FRAME_HASHES = ROOT / "tests" / "golden" / "frame_hashes.npz"
+
+
+def frame_parity(args, W, H, N, quality, use_assets, frame, index):
+    """One timed frame against the oracle's frame (tests/golden/frame_hashes.npz,
+    made by tests/golden/make_frame_hashes.py in the build container): sha256
+    of every RGBA8 row equal, and the frame hash over them. Only the inputs the
+    fixture was made with (the app's static camera, the reference's textures,
+    curved mode, noise mask off) have one."""
+    import numpy as np
+
+    fr = frame.cpu().numpy() if hasattr(frame, "cpu") else np.asarray(frame)
+    fr = np.ascontiguousarray(fr[:H])
+    rows_sha = np.stack([np.frombuffer(hashlib.sha256(fr[y].tobytes()).digest(), dtype=np.uint8) for y in range(H)])
+    digest = hashlib.sha256(rows_sha.tobytes()).hexdigest()
+    out = {"frame": index, "frame_sha": digest[:16], "frame_sha_match": None}
+    if not (args.camera == "static" and use_assets and args.mode == "curved" and args.percent_black < 0):
+        out["reason"] = "no oracle fixture for these inputs"
+        return out
+    if not FRAME_HASHES.exists():
+        out["reason"] = "tests/golden/frame_hashes.npz missing"
+        return out
+    with np.load(FRAME_HASHES) as z:
+        for cfg in ("c2", "c3", "c4", "c5"):
+            if f"{cfg}/config" not in z.files or tuple(int(v) for v in z[f"{cfg}/config"]) != (W, H, N):
+                continue
+            if bytes(z[f"{cfg}/skybox"]).decode() != quality:
+                continue
+            rows = z[f"{cfg}/rows"]
+            ok = bool(np.array_equal(rows_sha[rows], z[f"{cfg}/rgba_sha"]))
+            out.update(fixture=f"tests/golden/frame_hashes.npz {cfg}", rows_compared=int(len(rows)),
+                       rows_differing=int((rows_sha[rows] != z[f"{cfg}/rgba_sha"]).any(-1).sum()))
+            if f"{cfg}/frame_sha" in z.files:
+                ok = ok and digest == bytes(z[f"{cfg}/frame_sha"]).hex()
+            out["frame_sha_match"] = ok
+            return out
+    out["reason"] = "no oracle fixture for this size"
+    return out
 
 
 def load_matching(path, W, H, N, world):
@@ -564,16 +653,35 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
     }
 
 
+def cgroup_cpus():
+    """CPUs the cgroup's quota grants (cgroup v2 cpu.max, v1 cfs quota), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_cpu():
-    """(threads to use, nproc, CPU model): the box's CPU share is what
-    OMP_NUM_THREADS says there (16 per GPU); nproc counts the whole machine."""
+    """(threads, basis): every thread sched_getaffinity allows this process,
+    bounded by the cgroup's CPU quota when one is set (more threads than the
+    quota only time-slice), plus nproc and the CPU model for the line."""
     nproc = os.cpu_count() or 1
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = nproc
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    threads = min(aff, share) if share > 0 else aff
+    quota = cgroup_cpus()
+    threads = min(aff, quota) if quota else aff
     model = "unknown"
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -583,48 +691,88 @@ def host_cpu():
                 break
     except Exception:  # noqa: BLE001
         pass
-    return threads, nproc, model
+    return {"threads": threads, "affinity": aff, "cgroup_cpus": quota, "nproc": nproc, "model": model,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
 
 
-def cpu_baseline(cam, W, H, N, sample_rows):
-    """The reference's press-R CPU geodesic (src/main.cpp:73-124) swept over
-    a bounded sample of the frame's pixels: all threads of
-    this host's CPU share, -O2 (official) and -O0 (the reference's CMake
-    default), median of 3 runs each (oracle port)."""
+# BASELINE.json config 1: one press-R ray of 2000 steps from the app's camera
+# position (src/main.cpp:222), the directions SURVEY.md Appendix B timed
+PRESSR_RAYS = (((0.0, 2.0, 15.0), (1.0, -2.0, -15.0)), ((0.0, 2.0, 15.0), (3.0, -2.0, -15.0)))
+# the other sweeps of BASELINE.md §3: (name, width, height, max_steps)
+CPU_SWEEPS = (("640x360/1000", 640, 360, 1000), ("1920x1080/2000", 1920, 1080, 2000),
+              ("3840x2160/4000", 3840, 2160, 4000))
+
+
+def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
+    """The reference's press-R CPU geodesic (src/main.cpp:73-124, double
+    temporaries, a std::vector per ray) on this host (BASELINE.md §3), the
+    oracle's restatement of it ("port"; the reference app needs glm and GLFW,
+    absent here):
+      - value: swept over a bounded sample of this frame's rows (every pixel's
+        camera ray, N steps), all threads of host_cpu(), -O2, median of 3;
+      - O0: the same at -O0 (the reference's CMake default build);
+      - configs: config 1 (one ray at N = 2000, microseconds per ray on one
+        thread) and the 640x360 / 1000, 1920x1080 / 2000 and 3840x2160 / 4000
+        sweeps, each on a bounded row sample around the frame centre."""
     import statistics
+
+    import numpy as np
 
     import srpkg
 
     oracle = srpkg.load_oracle()
-    threads, nproc, model = host_cpu()
-    if sample_rows <= 0:
-        # calibrate: time 8 rows, size the sample to ~3 s per -O2 run
-        t = time.perf_counter()
-        oracle.pressr_sweep(cam, W, H, N, 2, H // 2 - 4, H // 2 + 4, threads)
-        dt = max(time.perf_counter() - t, 1e-3)
-        sample_rows = int(min(H, max(8, 8 * 3.0 / dt)))
+    hc = host_cpu()
+    threads = hc["threads"]
 
-    def rate(fn, rows):
-        y0 = max(0, H // 2 - rows // 2)  # rows [y0, y1) around the frame centre
-        y1 = min(H, y0 + rows)
-        runs = []
-        pts = 0
+    def rows_for(w, h, n, target_s):
+        t = time.perf_counter()  # calibrate on 8 rows through the centre
+        oracle.pressr_sweep(cam, w, h, n, 2, h // 2 - 4, h // 2 + 4, threads)
+        dt = max(time.perf_counter() - t, 1e-3)
+        return int(min(h, max(8, 8 * target_s / dt)))
+
+    def rate(fn, w, h, n, rows):
+        y0 = max(0, h // 2 - rows // 2)  # rows [y0, y1) around the frame centre
+        y1 = min(h, y0 + rows)
+        runs, pts = [], 0
         for _ in range(3):
             t = time.perf_counter()
-            pts = fn(cam, W, H, N, 2, y0, y1, threads)
+            pts = fn(cam, w, h, n, 2, y0, y1, threads)
             runs.append(time.perf_counter() - t)
         dt = statistics.median(runs)
-        return (y1 - y0) * W / dt / 1e6, y0, y1, pts, dt
+        return (y1 - y0) * w / dt / 1e6, y0, y1, pts, dt
 
-    v2, y0, y1, pts, dt = rate(oracle.pressr_sweep, sample_rows)
+    if sample_rows <= 0:
+        sample_rows = rows_for(W, H, N, budget_s)
+    v2, y0, y1, pts, dt = rate(oracle.pressr_sweep, W, H, N, sample_rows)
     o0 = None
     if hasattr(oracle, "pressr_sweep_O0"):
         try:
-            rows0 = max(8, sample_rows // 4)
-            v0, a0, b0, _, d0 = rate(oracle.pressr_sweep_O0, rows0)
+            v0, a0, b0, _, d0 = rate(oracle.pressr_sweep_O0, W, H, N, max(8, sample_rows // 4))
             o0 = {"value": round(v0, 4), "sample": f"rows [{a0},{b0}) x {W} px, median {d0:.2f} s"}
         except (FileNotFoundError, OSError):
             o0 = None
+    configs = {}
+    for pos, fwd in PRESSR_RAYS:  # config 1: microseconds per ray, one thread
+        v = np.array(fwd, dtype=np.float32)
+        v = (v * np.float32(1.0 / np.sqrt(np.float32(np.dot(v, v))))).tolist()
+        n_pts = oracle.pressr_ray_repeat(pos, v, 2000, 2, 1)
+        reps = 50
+        while True:
+            t = time.perf_counter()
+            oracle.pressr_ray_repeat(pos, v, 2000, 2, reps)
+            el = time.perf_counter() - t
+            if el > 0.3 or reps > 1 << 22:
+                break
+            reps *= 4
+        configs[f"config1 dir {fwd}"] = {"value": round(el / reps * 1e6, 3), "unit": "us/ray", "cores": 1,
+                                         "points": n_pts, "sample": f"{reps} traces, N = 2000, pos {pos}"}
+    for name, w, h, n in CPU_SWEEPS:
+        if (w, h, n) == (W, H, N):
+            configs[name] = {"value": round(v2, 4), "unit": "Mpixels/s", "cores": threads, "same_as": "value"}
+            continue
+        rv, a, b, p_, d = rate(oracle.pressr_sweep, w, h, n, rows_for(w, h, n, budget_s / 2))
+        configs[name] = {"value": round(rv, 4), "unit": "Mpixels/s", "cores": threads,
+                         "sample": f"rows [{a},{b}) x {w} px, {p_} points, median of 3 runs {d:.2f} s"}
     return {
         "value": round(v2, 4),
         "unit": "Mpixels/s",
@@ -632,9 +780,13 @@ def cpu_baseline(cam, W, H, N, sample_rows):
         "kind": "port",
         "sample": f"press-R loop (src/main.cpp:73-124) over rows [{y0},{y1}) x {W} px of the {W}x{H} frame, "
                   f"{N} steps, {pts} points, median of 3 runs {dt:.2f} s, -O2, {threads} threads",
-        "nproc": nproc,
-        "cpu_model": model,
+        "cores_basis": (f"sched_getaffinity allows {hc['affinity']} CPUs"
+                        + (f", the cgroup quota {hc['cgroup_cpus']}" if hc["cgroup_cpus"] else ", no cgroup quota")
+                        + f"; nproc {hc['nproc']}"),
+        "nproc": hc["nproc"],
+        "cpu_model": hc["model"],
         "O0": o0,
+        "configs": configs,
         "note": "integrator only: the press-R loop does no scene intersection or shading (BASELINE.md §3)",
     }
 

@@ -55,6 +55,8 @@ def load() -> C.CDLL:
         lib.sro_pressr_sweep.restype = C.c_int64
         lib.sro_pressr_sweep.argtypes = [C.POINTER(abi.Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int]
+        lib.sro_pressr_ray_repeat.restype = C.c_int
+        lib.sro_pressr_ray_repeat.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int]
         _lib = lib
     return _lib
 
@@ -111,6 +113,14 @@ def test_ray_points(pos, forward, max_steps, max_revolutions=2):
     n = lib.sro_test_ray_points((C.c_float * 3)(*pos), (C.c_float * 3)(*forward), max_steps, max_revolutions,
                                 buf, cap)
     return [(buf[3 * i], buf[3 * i + 1], buf[3 * i + 2]) for i in range(min(n, cap))]
+
+
+def pressr_ray_repeat(pos, forward, max_steps, max_revolutions=2, reps=1) -> int:
+    """One press-R ray (a std::vector of points per trace, src/main.cpp:94-124)
+    traced `reps` times on the calling thread; returns its point count."""
+    lib = load()
+    return int(lib.sro_pressr_ray_repeat((C.c_float * 3)(*pos), (C.c_float * 3)(*forward), max_steps,
+                                         max_revolutions, reps))
 
 
 _lib_O0 = None

@@ -948,6 +948,23 @@ int sro_test_ray_points(const float pos[3], const float forward[3], int max_step
     return c1_trace(origin, dir, max_steps, max_revolutions, out_xyz, max_points, NULL, NULL);
 }
 
+/* BASELINE config 1: one press-R ray (src/main.cpp:94-124, a std::vector of
+ * points per call) traced `reps` times on this thread, for a per-ray time.
+ * Returns the points of one trace. */
+int sro_pressr_ray_repeat(const float pos[3], const float forward[3], int max_steps, int max_revolutions,
+                          int reps) {
+    v3 dir = load_v3(forward);
+    v3 origin = add3(load_v3(pos), scl3(dir, 1.0f));
+    int n = 0;
+    for (int k = 0; k < reps; k++) {
+        v3* vec = NULL;
+        int cap = 0;
+        n = c1_trace(origin, dir, max_steps, max_revolutions, NULL, 0, &vec, &cap);
+        free(vec);
+    }
+    return n;
+}
+
 typedef struct {
     const sr_camera* cam;
     int W, H, row_begin, row_end, tid, nthreads, max_steps, max_revolutions;

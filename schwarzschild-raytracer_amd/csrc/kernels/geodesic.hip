@@ -1815,7 +1815,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     sr_lds_ev[threadIdx.x >> 6] += 1;
                 // a new frame (reseed): the cylinders' direction tests start over
                 SR_PT(2);
-#ifdef SR_STATS_BH  // measurement only: the black hole's triggering lanes by orbit state
+#ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
                 {
                     const bool h0 = !(bs.T < bs.E[0]);
                     const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
@@ -1849,21 +1849,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(29, __popcll(__ballot(any && outw)));
                     SR_STAT(30, __popcll(__ballot(any && inc)));
                     SR_STAT(31, __popcll(__ballot(any)));
-                }
-#endif
-#ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
-                {
-                    const bool h0 = !(bs.T < bs.E[0]);
-                    const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
-                    SR_STAT(23, __popcll(__ballot(h0 && r.u > 1.0f)));
-                    SR_STAT(24, __popcll(__ballot(h0 && r.u <= 1.0f && r.u > 0.9f)));
-                    SR_STAT(25, __popcll(__ballot(h0 && ring)));
-                    SR_STAT(26, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && r.du > 0.0f)));
-                    SR_STAT(27, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && !(r.du > 0.0f))));
-                    SR_STAT(28, __popcll(__ballot(event)));
-                    SR_STAT(29, __popcll(__ballot(h0)));
-                    SR_STAT(30, __ballot(h0) != 0ull);
-                    SR_STAT(31, __popcll(__ballot(1)));
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
@@ -2129,9 +2114,18 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
     __shared__ int offs[256];
     __shared__ int nsplit;
     const int t = threadIdx.x;
+    // 256 cost buckets, descending cost = descending bucket. With split
+    // tiles the split threshold is a bucket boundary (costs >= split_min in
+    // 128..255, below it in 0..127), so exactly the tiles of cost >=
+    // split_min may be split; without, the buckets span [0, max_cost].
+    const int smin = split_min < 1 ? 1 : split_min;
     auto bucket = [&](int c) {
-        long long b = (long long)(c < 0 ? 0 : c) * 256 / ((long long)max_cost + 1);
-        return (int)(b > 255 ? 255 : b);
+        c = c < 0 ? 0 : c;
+        long long b;
+        if (split_tiles == 0) b = (long long)c * 256 / ((long long)max_cost + 1);
+        else if (c >= smin) b = 128 + (long long)(c - smin) * 128 / ((long long)(max_cost > smin ? max_cost : smin) - smin + 1);
+        else b = (long long)c * 128 / smin;
+        return (int)(b < 0 ? 0 : b > 255 ? 255 : b);
     };
     if (t < 256) hist[t] = 0;
     __syncthreads();
@@ -2139,11 +2133,10 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
     __syncthreads();
     if (t == 0) {
         int run = 0, hi = 0;
-        const int bmin = bucket(split_min < 1 ? 1 : split_min);
         for (int b = 255; b >= 0; b--) {
             offs[b] = run;
             run += hist[b];
-            if (b >= bmin) hi += hist[b];
+            if (b >= 128) hi += hist[b];
         }
         nsplit = split_tiles < hi ? split_tiles : hi;
     }

@@ -33,7 +33,14 @@ constexpr float kPi = 3.1415926535f;  // frag:10
 struct Table {
     float4* dev = nullptr;
     int steps = 0;
+    std::vector<float4> host;  // source of the stream-ordered upload, kept until the entry goes
+    uint64_t used = 0;
 };
+
+// Device caches of a context (step tables, launch orders, block lists) hold at
+// most this many entries each; the least recently used goes, its buffers
+// freed in stream order after the context's in-flight frames.
+constexpr size_t kCacheEntries = 8;
 
 }  // namespace
 
@@ -63,11 +70,23 @@ struct sr_ctx {
     struct Order {
         int* order = nullptr;
         int* cost = nullptr;
+        std::vector<int> host;  // source of the stream-ordered upload
+        uint64_t used = 0;
     };
-    // (gx, gy, split_tiles, split_log2, block list): a block list's tiles have their own costs
+    // (gx, gy, split_tiles, split_log2, block list): a block list's tiles have
+    // their own costs; the list is its device copy, one per distinct content
     std::map<std::tuple<int, int, int, int, const int*>, Order> orders;
     // device copies of the block lists of sr_render_block_list, by content
-    std::map<std::vector<int>, int*> block_lists;
+    // (the key is the upload's source)
+    struct BlockList {
+        int* dev = nullptr;
+        uint64_t used = 0;
+    };
+    std::map<std::vector<int>, BlockList> block_lists;
+    uint64_t tick = 0;  // LRU clock of the caches
+    // synchronous uploads (sr_set_*) run on this non-blocking stream, never
+    // on the null stream (which would wait for other contexts' work)
+    hipStream_t upload = nullptr;
     // split tiles (sr_set_split): 0 = off
     int split_tiles = 0, split_log2 = 4, split_min_steps = 1;
     const int* last_order = nullptr;  // the launch codes of the context's last frame (its next frame's order)
@@ -286,10 +305,34 @@ void test_ray_frame(V3 d, float* axes9) {
 
 inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
 
-int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
+// Frees a device buffer in stream order: after the context's in-flight
+// frames (its last launch stream; `s` before its first launch). hipFree would
+// synchronise the whole device.
+void release(sr_ctx* ctx, void* p, hipStream_t s) {
+    if (p) (void)hipFreeAsync(p, ctx->launched ? ctx->last_stream : s);
+}
+
+// LRU eviction down to kCacheEntries - 1 entries (one is about to be added).
+template <class Map, class Free>
+void evict_lru(sr_ctx* ctx, Map& m, Free&& free_entry) {
+    while (m.size() >= kCacheEntries) {
+        auto victim = m.begin();
+        for (auto it = m.begin(); it != m.end(); ++it)
+            if (it->second.used < victim->second.used) victim = it;
+        free_entry(victim->second);
+        m.erase(victim);
+    }
+}
+
+void evict_tables(sr_ctx* ctx) {
+    evict_lru(ctx, ctx->tables, [&](Table& t) { release(ctx, t.dev, ctx->last_stream); });
+}
+
+int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const float4** out) {
     auto key = std::make_pair(max_steps, max_revs);
     auto it = ctx->tables.find(key);
     if (it != ctx->tables.end()) {
+        it->second.used = ++ctx->tick;
         *out = it->second.dev;
         return SR_OK;
     }
@@ -322,19 +365,40 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, const float4** out) {
         c1 = c;
         s1 = sn;
     }
-    Table t;
+    evict_tables(ctx);
+    Table& t = ctx->tables[key];
     t.steps = max_steps;
-    if (!hip_ok(hipMalloc(&t.dev, h.size() * sizeof(float4)))) return SR_E_NOMEM;
-    if (!hip_ok(hipMemcpy(t.dev, h.data(), h.size() * sizeof(float4), hipMemcpyHostToDevice))) {
-        (void)hipFree(t.dev);
+    t.host = std::move(h);
+    t.used = ++ctx->tick;
+    // stream-ordered: allocated and filled on the caller's stream, ahead of
+    // the launch that reads it (no device-wide synchronisation)
+    if (!hip_ok(hipMallocAsync(reinterpret_cast<void**>(&t.dev), t.host.size() * sizeof(float4), s))) {
+        ctx->tables.erase(key);
+        return SR_E_NOMEM;
+    }
+    if (!hip_ok(hipMemcpyAsync(t.dev, t.host.data(), t.host.size() * sizeof(float4), hipMemcpyHostToDevice, s))) {
+        release(ctx, t.dev, s);
+        ctx->tables.erase(key);
         return SR_E_HIP;
     }
-    ctx->tables[key] = t;
     *out = t.dev;
     return SR_OK;
 }
 
-int upload_rgba(const uint8_t* px, int w, int h, int layers, int ch, uint32_t** dev) {
+// Synchronous upload of host bytes into a fresh device buffer on the
+// context's private upload stream (the previous buffer is freed in stream
+// order after the context's in-flight frames).
+int upload_bytes(sr_ctx* ctx, const void* src, size_t bytes, void** dev) {
+    release(ctx, *dev, ctx->upload);
+    *dev = nullptr;
+    if (!hip_ok(hipMallocAsync(dev, bytes, ctx->upload))) return SR_E_NOMEM;
+    if (!hip_ok(hipMemcpyAsync(*dev, src, bytes, hipMemcpyHostToDevice, ctx->upload)) ||
+        !hip_ok(hipStreamSynchronize(ctx->upload)))
+        return SR_E_HIP;
+    return SR_OK;
+}
+
+int upload_rgba(sr_ctx* ctx, const uint8_t* px, int w, int h, int layers, int ch, uint32_t** dev) {
     size_t n = (size_t)w * h * layers;
     std::vector<uint32_t> rgba(n);
     for (size_t i = 0; i < n; i++) {
@@ -342,23 +406,7 @@ int upload_rgba(const uint8_t* px, int w, int h, int layers, int ch, uint32_t** 
         uint32_t a = ch == 4 ? p[3] : 255u;  // GL_RGB reads alpha 1
         rgba[i] = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | (a << 24);
     }
-    if (*dev) {
-        (void)hipFree(*dev);
-        *dev = nullptr;
-    }
-    if (!hip_ok(hipMalloc(dev, n * sizeof(uint32_t)))) return SR_E_NOMEM;
-    if (!hip_ok(hipMemcpy(*dev, rgba.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice))) return SR_E_HIP;
-    return SR_OK;
-}
-
-void free_pixel_state(sr_ctx* ctx) {
-    if (ctx->d_ps) (void)hipFree(ctx->d_ps);
-    if (ctx->d_list) (void)hipFree(ctx->d_list);
-    if (ctx->d_count) (void)hipFree(ctx->d_count);
-    ctx->d_ps = nullptr;
-    ctx->d_list = nullptr;
-    ctx->d_count = nullptr;
-    ctx->ps_n = 0;
+    return upload_bytes(ctx, rgba.data(), n * sizeof(uint32_t), reinterpret_cast<void**>(dev));
 }
 
 // Waits for this context's in-flight frames (its last launch stream), not
@@ -368,19 +416,32 @@ bool wait_ctx(sr_ctx* ctx) {
     return hip_ok(hipStreamSynchronize(ctx->last_stream));
 }
 
-int ensure_pixel_state(sr_ctx* ctx, size_t n) {
+void free_pixel_state(sr_ctx* ctx, hipStream_t s) {
+    release(ctx, ctx->d_ps, s);
+    release(ctx, ctx->d_list, s);
+    release(ctx, ctx->d_count, s);
+    ctx->d_ps = nullptr;
+    ctx->d_list = nullptr;
+    ctx->d_count = nullptr;
+    ctx->ps_n = 0;
+}
+
+// Grows the pixel-state planes in stream order: the old buffers are freed
+// after the context's in-flight frames, the new ones allocated and cleared
+// on the caller's stream ahead of the launch (no host wait, no device-wide
+// synchronisation).
+int ensure_pixel_state(sr_ctx* ctx, size_t n, hipStream_t s) {
     if (n <= ctx->ps_n) return SR_OK;
-    // growing: wait for this context's in-flight frames that use the old buffers
-    if (ctx->ps_n && !wait_ctx(ctx)) return SR_E_HIP;
-    free_pixel_state(ctx);
-    if (!hip_ok(hipMalloc(&ctx->d_ps, n * SR_PS_FIELDS * sizeof(float))) ||
-        !hip_ok(hipMalloc(&ctx->d_list, n * sizeof(int))) || !hip_ok(hipMalloc(&ctx->d_count, 2 * sizeof(int)))) {
-        free_pixel_state(ctx);
+    free_pixel_state(ctx, s);
+    if (!hip_ok(hipMallocAsync(reinterpret_cast<void**>(&ctx->d_ps), n * SR_PS_FIELDS * sizeof(float), s)) ||
+        !hip_ok(hipMallocAsync(reinterpret_cast<void**>(&ctx->d_list), n * sizeof(int), s)) ||
+        !hip_ok(hipMallocAsync(reinterpret_cast<void**>(&ctx->d_count), 2 * sizeof(int), s))) {
+        free_pixel_state(ctx, s);
         return SR_E_NOMEM;
     }
     // [0]: the shade kernel's resume queue
-    if (!hip_ok(hipMemset(ctx->d_count, 0, 2 * sizeof(int)))) {
-        free_pixel_state(ctx);
+    if (!hip_ok(hipMemsetAsync(ctx->d_count, 0, 2 * sizeof(int), s))) {
+        free_pixel_state(ctx, s);
         return SR_E_HIP;
     }
     ctx->ps_n = n;
@@ -392,11 +453,7 @@ int ensure_pixel_state(sr_ctx* ctx, size_t n) {
 // +-SR_OPQ_RADIUS of (x, y), wrapping like the sampler, has alpha 255. A
 // bilinear footprint {x0, x0 + 1} x {y0, y0 + 1} whose floor lies within one
 // texel of (x, y) then reads alpha 1 exactly (LERP filtering).
-int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_t** dev) {
-    if (*dev) {
-        (void)hipFree(*dev);
-        *dev = nullptr;
-    }
+int make_opacity_map(sr_ctx* ctx, const uint8_t* px, int w, int h, int layers, int ch, uint8_t** dev) {
     const size_t stride = ((size_t)w + 7) / 8;
     std::vector<uint8_t> bits(stride * (size_t)h * (size_t)layers, 0);
     std::vector<uint8_t> row((size_t)w * h);
@@ -420,9 +477,18 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
                 if (m) bits[((size_t)l * h + y) * stride + (x >> 3)] |= (uint8_t)(1u << (x & 7));
             }
     }
-    if (!hip_ok(hipMalloc(dev, bits.size()))) return SR_E_NOMEM;
-    if (!hip_ok(hipMemcpy(*dev, bits.data(), bits.size(), hipMemcpyHostToDevice))) return SR_E_HIP;
-    return SR_OK;
+    return upload_bytes(ctx, bits.data(), bits.size(), reinterpret_cast<void**>(dev));
+}
+
+void evict_orders(sr_ctx* ctx) {
+    evict_lru(ctx, ctx->orders, [&](sr_ctx::Order& o) {
+        if (ctx->last_order == o.order) {
+            ctx->last_order = nullptr;
+            ctx->last_slots = 0;
+        }
+        release(ctx, o.order, ctx->last_stream);
+        release(ctx, o.cost, ctx->last_stream);
+    });
 }
 
 // Launch order for a grid shape: tiles nearest the frame centre first (where
@@ -430,11 +496,12 @@ int make_opacity_map(const uint8_t* px, int w, int h, int layers, int ch, uint8_
 // buffer pair per shape and split setting, allocated on first use. Entries
 // are launch codes (geodesic.hip sr_order_kernel): tile << 8 for a whole
 // tile, -1 for the split grid's slots no tile uses yet.
-int ensure_order(sr_ctx* ctx, int gx, int gy, const int* list, int** order, int** cost) {
+int ensure_order(sr_ctx* ctx, int gx, int gy, const int* list, hipStream_t s, int** order, int** cost) {
     const int split = ctx->split_tiles;
     const auto key = std::make_tuple(gx, gy, split, split ? ctx->split_log2 : 0, list);
     auto it = ctx->orders.find(key);
     if (it != ctx->orders.end()) {
+        it->second.used = ++ctx->tick;
         *order = it->second.order;
         *cost = it->second.cost;
         return SR_OK;
@@ -451,18 +518,24 @@ int ensure_order(sr_ctx* ctx, int gx, int gy, const int* list, int** order, int*
     std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return d[a] < d[b]; });
     for (int& v : ord) v <<= 8;
     ord.resize(slots, -1);
-    sr_ctx::Order o;
-    if (!hip_ok(hipMalloc(&o.order, slots * sizeof(int))) || !hip_ok(hipMalloc(&o.cost, n * sizeof(int)))) {
-        if (o.order) (void)hipFree(o.order);
+    evict_orders(ctx);
+    sr_ctx::Order& o = ctx->orders[key];
+    o.host = std::move(ord);
+    o.used = ++ctx->tick;
+    // stream-ordered, on the caller's stream ahead of the launch
+    if (!hip_ok(hipMallocAsync(reinterpret_cast<void**>(&o.order), slots * sizeof(int), s)) ||
+        !hip_ok(hipMallocAsync(reinterpret_cast<void**>(&o.cost), n * sizeof(int), s))) {
+        release(ctx, o.order, s);
+        ctx->orders.erase(key);
         return SR_E_NOMEM;
     }
-    if (!hip_ok(hipMemcpy(o.order, ord.data(), slots * sizeof(int), hipMemcpyHostToDevice)) ||
-        !hip_ok(hipMemset(o.cost, 0, n * sizeof(int)))) {
-        (void)hipFree(o.order);
-        (void)hipFree(o.cost);
+    if (!hip_ok(hipMemcpyAsync(o.order, o.host.data(), slots * sizeof(int), hipMemcpyHostToDevice, s)) ||
+        !hip_ok(hipMemsetAsync(o.cost, 0, n * sizeof(int), s))) {
+        release(ctx, o.order, s);
+        release(ctx, o.cost, s);
+        ctx->orders.erase(key);
         return SR_E_HIP;
     }
-    ctx->orders[key] = o;
     *order = o.order;
     *cost = o.cost;
     return SR_OK;
@@ -475,20 +548,43 @@ int ensure_block_list(sr_ctx* ctx, const int* blocks, int n, hipStream_t s, cons
     std::vector<int> key(blocks, blocks + n);
     auto it = ctx->block_lists.find(key);
     if (it != ctx->block_lists.end()) {
-        *dev = it->second;
+        it->second.used = ++ctx->tick;
+        *dev = it->second.dev;
         return SR_OK;
     }
-    int* d = nullptr;
-    if (!hip_ok(hipMalloc(&d, (size_t)n * sizeof(int)))) return SR_E_NOMEM;
-    // ordered before this context's launches on its stream; synchronized once
-    // so that the host copy of the list may go
-    if (!hip_ok(hipMemcpyAsync(d, key.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, s)) ||
-        !hip_ok(hipStreamSynchronize(s))) {
-        (void)hipFree(d);
+    if (ctx->block_lists.size() >= kCacheEntries) {
+        // an evicted list's launch orders go with it (they are keyed by its device copy)
+        evict_lru(ctx, ctx->block_lists, [&](sr_ctx::BlockList& b) {
+            for (auto o = ctx->orders.begin(); o != ctx->orders.end();) {
+                if (std::get<4>(o->first) == b.dev) {
+                    if (ctx->last_order == o->second.order) {
+                        ctx->last_order = nullptr;
+                        ctx->last_slots = 0;
+                    }
+                    release(ctx, o->second.order, ctx->last_stream);
+                    release(ctx, o->second.cost, ctx->last_stream);
+                    o = ctx->orders.erase(o);
+                } else {
+                    ++o;
+                }
+            }
+            release(ctx, b.dev, ctx->last_stream);
+        });
+    }
+    // the map's key is the source of the stream-ordered upload: it lives as long as the entry
+    auto ins = ctx->block_lists.emplace(std::move(key), sr_ctx::BlockList{});
+    sr_ctx::BlockList& b = ins.first->second;
+    b.used = ++ctx->tick;
+    if (!hip_ok(hipMallocAsync(reinterpret_cast<void**>(&b.dev), (size_t)n * sizeof(int), s))) {
+        ctx->block_lists.erase(ins.first);
+        return SR_E_NOMEM;
+    }
+    if (!hip_ok(hipMemcpyAsync(b.dev, ins.first->first.data(), (size_t)n * sizeof(int), hipMemcpyHostToDevice, s))) {
+        release(ctx, b.dev, s);
+        ctx->block_lists.erase(ins.first);
         return SR_E_HIP;
     }
-    ctx->block_lists[std::move(key)] = d;
-    *dev = d;
+    *dev = b.dev;
     return SR_OK;
 }
 
@@ -564,21 +660,21 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.block_list = d_block_list;
     fr.wave_cost = d_wave_cost;
     if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const float4* tbl = nullptr;
-    rc = ensure_table(ctx, params->max_steps, params->max_revolutions, &tbl);
+    rc = ensure_table(ctx, params->max_steps, params->max_revolutions, s, &tbl);
     if (rc != SR_OK) return rc;
-    rc = ensure_pixel_state(ctx, (size_t)fr.tiles * (size_t)n_frames * 256);
+    rc = ensure_pixel_state(ctx, (size_t)fr.tiles * (size_t)n_frames * 256, s);
     if (rc != SR_OK) return rc;
     int* order = nullptr;
     int* cost = nullptr;
     if (nrows > 0) {
-        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, d_block_list, &order, &cost);
+        rc = ensure_order(ctx, (width + 15) / 16, (nrows + 15) / 16, d_block_list, s, &order, &cost);
         if (rc != SR_OK) return rc;
         ctx->last_order = order;
         ctx->last_slots = (size_t)((width + 15) / 16) * (size_t)((nrows + 15) / 16) +
                           (size_t)((64 >> (ctx->split_tiles ? ctx->split_log2 : 6)) - 1) * (size_t)ctx->split_tiles;
     }
-    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
                                       dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count, order, cost,
                                       ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
@@ -619,13 +715,20 @@ int sr_create(sr_ctx** out, int hip_device) {
     if (!c) return SR_E_NOMEM;
     c->device = hip_device;
     std::memset(&c->h_scene, 0, sizeof c->h_scene);
+    if (!hip_ok(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking))) {
+        c->upload = nullptr;
+        sr_destroy(c);
+        return SR_E_HIP;
+    }
     if (!hip_ok(hipMalloc(&c->d_scene, sizeof(sr_dev_scene))) ||
         !hip_ok(hipMalloc(&c->d_segs, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float)))) {
         sr_destroy(c);
         return SR_E_NOMEM;
     }
-    if (!hip_ok(hipMemset(c->d_scene, 0, sizeof(sr_dev_scene))) ||
-        !hip_ok(hipMemset(c->d_segs, 0, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float)))) {
+    if (!hip_ok(hipMemsetAsync(c->d_scene, 0, sizeof(sr_dev_scene), c->upload)) ||
+        !hip_ok(hipMemsetAsync(c->d_segs, 0, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float),
+                               c->upload)) ||
+        !hip_ok(hipStreamSynchronize(c->upload))) {
         sr_destroy(c);
         return SR_E_HIP;
     }
@@ -646,16 +749,24 @@ void sr_destroy(sr_ctx* c) {
     (void)wait_ctx(c);
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_segs) (void)hipFree(c->d_segs);
-    if (c->d_bg) (void)hipFree(c->d_bg);
-    if (c->d_arr) (void)hipFree(c->d_arr);
-    if (c->d_opq) (void)hipFree(c->d_opq);
-    for (auto& kv : c->tables) (void)hipFree(kv.second.dev);
-    free_pixel_state(c);
-    for (auto& kv : c->orders) {
-        (void)hipFree(kv.second.order);
-        (void)hipFree(kv.second.cost);
+    // the rest came from the stream-ordered allocator: freed the same way,
+    // then waited for (the context's frames are done: wait_ctx)
+    const hipStream_t s = c->upload;
+    if (s) {
+        c->launched = false;  // release() frees on `s`
+        release(c, c->d_bg, s);
+        release(c, c->d_arr, s);
+        release(c, c->d_opq, s);
+        for (auto& kv : c->tables) release(c, kv.second.dev, s);
+        free_pixel_state(c, s);
+        for (auto& kv : c->orders) {
+            release(c, kv.second.order, s);
+            release(c, kv.second.cost, s);
+        }
+        for (auto& kv : c->block_lists) release(c, kv.second.dev, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
     }
-    for (auto& kv : c->block_lists) (void)hipFree(kv.second);
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
     delete c;
 }
@@ -663,7 +774,7 @@ void sr_destroy(sr_ctx* c) {
 int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {
     if (!c || !px || w <= 0 || h <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
-    int rc = upload_rgba(px, w, h, 1, ch, &c->d_bg);
+    int rc = upload_rgba(c, px, w, h, 1, ch, &c->d_bg);
     if (rc != SR_OK) {
         c->bg_w = c->bg_h = 0;
         return rc;
@@ -676,8 +787,8 @@ int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {
 int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers, int ch) {
     if (!c || !px || w <= 0 || h <= 0 || layers <= 0 || (ch != 3 && ch != 4)) return SR_E_INVALID;
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
-    int rc = upload_rgba(px, w, h, layers, ch, &c->d_arr);
-    if (rc == SR_OK) rc = make_opacity_map(px, w, h, layers, ch, &c->d_opq);
+    int rc = upload_rgba(c, px, w, h, layers, ch, &c->d_arr);
+    if (rc == SR_OK) rc = make_opacity_map(c, px, w, h, layers, ch, &c->d_opq);
     if (rc != SR_OK) {
         c->arr_w = c->arr_h = c->arr_layers = 0;
         return rc;
@@ -768,7 +879,9 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
     std::memcpy(d.texture_sizes, s->texture_sizes, sizeof d.texture_sizes);
     std::memcpy(d.max_texture_size, s->max_texture_size, sizeof d.max_texture_size);
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
-    if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
+    if (!hip_ok(hipMemcpyAsync(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice, c->upload)) ||
+        !hip_ok(hipStreamSynchronize(c->upload)))
+        return SR_E_HIP;
     c->h_scene = d;
     c->scene_set = true;
     return SR_OK;
@@ -804,9 +917,11 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
     }
     d.tr_num_segments = nseg;
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
-    if (!hip_ok(hipMemcpy(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice)))
+    if (!hip_ok(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice,
+                               c->upload)) ||
+        !hip_ok(hipMemcpyAsync(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice, c->upload)) ||
+        !hip_ok(hipStreamSynchronize(c->upload)))
         return SR_E_HIP;
-    if (!hip_ok(hipMemcpy(c->d_scene, &d, sizeof d, hipMemcpyHostToDevice))) return SR_E_HIP;
     c->h_scene = d;
     return SR_OK;
 }
@@ -917,7 +1032,9 @@ int sr_debug_last_order(sr_ctx* c, int* out, int max_n, int* n) {
     if (!c->last_order) return SR_OK;
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     const size_t k = c->last_slots < (size_t)max_n ? c->last_slots : (size_t)max_n;
-    if (k && !hip_ok(hipMemcpy(out, c->last_order, k * sizeof(int), hipMemcpyDeviceToHost))) return SR_E_HIP;
+    if (k && (!hip_ok(hipMemcpyAsync(out, c->last_order, k * sizeof(int), hipMemcpyDeviceToHost, c->upload)) ||
+              !hip_ok(hipStreamSynchronize(c->upload))))
+        return SR_E_HIP;
     return SR_OK;
 }
 

@@ -12,6 +12,7 @@ import srpkg  # noqa: E402
 
 GOLDEN = ROOT / "tests" / "golden" / "golden.npz"
 GOLDEN_R2 = ROOT / "tests" / "golden" / "golden_r2.npz"  # reseed, config 2, material flags
+GOLDEN_R3 = ROOT / "tests" / "golden" / "golden_r3.npz"  # bands of the headline-size frames
 
 
 class Golden:
@@ -56,7 +57,7 @@ def oracle():
 def golden():
     if not GOLDEN.exists() or not GOLDEN_R2.exists():
         pytest.skip("golden fixtures missing (python tests/golden/make_golden.py [--set r2])")
-    return Golden([GOLDEN, GOLDEN_R2])
+    return Golden([GOLDEN, GOLDEN_R2] + ([GOLDEN_R3] if GOLDEN_R3.exists() else []))
 
 
 @pytest.fixture(scope="session")
@@ -92,3 +93,12 @@ def load_case(pkg, golden, name):
     tr = sc.struct_from_bytes(abi.TestRay, golden[name + "/test_ray"])
     w, h = (int(v) for v in golden[name + "/size"])
     return scene, cam, params, tr, w, h
+
+
+def case_rows(golden, name, height):
+    """(row_begin, row_end) a golden case holds: a band of the frame (the
+    round-3 headline-size goldens) or the whole frame."""
+    if name + "/rows" in golden:
+        y0, y1 = (int(v) for v in golden[name + "/rows"])
+        return y0, y1
+    return 0, height

@@ -21,6 +21,7 @@ the C++ mirror of src/main.cpp:222-268) and integer-procedural textures, so the
 goldens do not depend on a JPEG decoder. Run in the build container:
     python tests/golden/make_golden.py            # writes tests/golden/golden.npz
     python tests/golden/make_golden.py --set r2   # writes tests/golden/golden_r2.npz
+    python tests/golden/make_golden.py --set r3   # writes tests/golden/golden_r3.npz (headline-size bands)
 """
 from __future__ import annotations
 
@@ -56,6 +57,7 @@ GL_TEXTURE_WRAP_S, GL_TEXTURE_WRAP_T, GL_REPEAT = 0x2802, 0x2803, 0x2901
 GL_TEXTURE_MIN_FILTER, GL_TEXTURE_MAG_FILTER, GL_LINEAR = 0x2801, 0x2800, 0x2601
 GL_COLOR_BUFFER_BIT, GL_UNPACK_ALIGNMENT, GL_PACK_ALIGNMENT = 0x4000, 0x0CF5, 0x0D05
 GL_FRAMEBUFFER, GL_RENDERBUFFER, GL_COLOR_ATTACHMENT0, GL_FRAMEBUFFER_COMPLETE = 0x8D40, 0x8D41, 0x8CE0, 0x8CD5
+GL_SCISSOR_TEST = 0x0C11
 
 ES_CAPACITIES = {
     "MAX_LIGHTS": 1, "MAX_TEXTURES": 2, "MAX_MATERIALS": 3, "MAX_SPHERES": 1, "MAX_PLANES": 1,
@@ -337,7 +339,9 @@ class SwiftShader:
             gl.glTexParameteri(target, GL_TEXTURE_MIN_FILTER, GL_LINEAR)
             gl.glTexParameteri(target, GL_TEXTURE_MAG_FILTER, GL_LINEAR)
 
-    def draw(self, prog, width, height, float_target=False):
+    def draw(self, prog, width, height, float_target=False, rows=None):
+        """The full-screen draw; rows=(y0, y1): only that band of the frame is
+        rasterised (scissor test) and read back."""
         gl = self.gl
         fbo, rb = C.c_uint(), C.c_uint()
         gl.glGenFramebuffers(1, C.byref(fbo))
@@ -351,29 +355,35 @@ class SwiftShader:
         gl.glViewport(0, 0, width, height)
         gl.glClearColor(C.c_float(0), C.c_float(0), C.c_float(0), C.c_float(0))
         gl.glClear(GL_COLOR_BUFFER_BIT)
+        y0, y1 = rows if rows else (0, height)
+        if rows:
+            gl.glEnable(GL_SCISSOR_TEST)
+            gl.glScissor(0, y0, width, y1 - y0)
         gl.glUseProgram(prog)
         gl.glDrawElements(GL_TRIANGLES, 6, GL_UNSIGNED_INT, None)
         gl.glFinish()
+        if rows:
+            gl.glDisable(GL_SCISSOR_TEST)
         err = gl.glGetError()
         if err:
             raise RuntimeError(f"GL error 0x{err:x}")
         gl.glPixelStorei(GL_PACK_ALIGNMENT, 1)
         if float_target:
-            out = np.zeros((height, width, 4), dtype=np.float32)
-            gl.glReadPixels(0, 0, width, height, GL_RGBA, GL_FLOAT, out.ctypes.data_as(C.c_void_p))
+            out = np.zeros((y1 - y0, width, 4), dtype=np.float32)
+            gl.glReadPixels(0, y0, width, y1 - y0, GL_RGBA, GL_FLOAT, out.ctypes.data_as(C.c_void_p))
         else:
-            out = np.zeros((height, width, 4), dtype=np.uint8)
-            gl.glReadPixels(0, 0, width, height, GL_RGBA, GL_UNSIGNED_BYTE, out.ctypes.data_as(C.c_void_p))
+            out = np.zeros((y1 - y0, width, 4), dtype=np.uint8)
+            gl.glReadPixels(0, y0, width, y1 - y0, GL_RGBA, GL_UNSIGNED_BYTE, out.ctypes.data_as(C.c_void_p))
         gl.glDeleteFramebuffers(1, C.byref(fbo))
         gl.glDeleteRenderbuffers(1, C.byref(rb))
         return out  # rows bottom-up (GL order), like the kernel's output
 
     def render(self, scene, cam, params, width, height, test_ray=None, steps_variant=False, float_target=False,
-               profile="default"):
+               profile="default", rows=None):
         prog = self.program(steps_variant, profile)
         tr = test_ray if test_ray is not None else abi.default_test_ray()
         self.set_uniforms(prog, scene, cam, params, tr, width, height, ES_PROFILES[profile])
-        return self.draw(prog, width, height, float_target)
+        return self.draw(prog, width, height, float_target, rows)
 
 
 # ---- the golden case list ----------------------------------------------------------
@@ -463,6 +473,27 @@ def cases_r2():
     return out
 
 
+def cases_r3():
+    """Round-3 goldens (golden_r3.npz): bands of the headline frame itself
+    (BASELINE config 3, 1920x1080 / 2000 steps, the app's camera) where its
+    cost is - rows 704-719 hold the photon-ring waves that set the frame's
+    critical path (bench roofline.critical_path), rows 536-551 run through the
+    black hole - for the untextured and the textured default scene, and a
+    3840-wide band of config 4 (4000 steps) through the ring. Each band is the
+    full-size frame rasterised under a scissor rectangle: uv, resolution and
+    every ray are the full frame's."""
+    P = abi.default_params
+    dcam = abi.default_camera()
+    out = []
+    for y0 in (704, 536):
+        for kind in ("untex", "tex"):
+            out.append((f"band1080_{y0}_{kind}", kind, dcam, P(max_steps=2000, percent_black=-1.0), 1920, 1080, None,
+                        {"steps": True, "rows": (y0, y0 + 16)}))
+    out.append(("band2160_1408_untex", "untex", dcam, P(max_steps=4000, percent_black=-1.0), 3840, 2160, None,
+                {"steps": True, "rows": (1408, 1424)}))
+    return out
+
+
 def scene_for(kind, sizes, mx):
     if kind == "features":
         return sc.scene_features()
@@ -486,19 +517,21 @@ def texture_set(kind):
 
 def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--set", choices=["r1", "r2"], default="r1",
-                    help="r1: golden.npz (round-1 cases); r2: golden_r2.npz (reseed, config 2, material flags)")
+    ap.add_argument("--set", choices=["r1", "r2", "r3"], default="r1",
+                    help="r1: golden.npz (round-1 cases); r2: golden_r2.npz (reseed, config 2, material flags); "
+                         "r3: golden_r3.npz (bands of the headline-size frames)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--only", default=None)
     args = ap.parse_args(argv)
-    out_path = args.out or str(Path(__file__).resolve().parent / ("golden.npz" if args.set == "r1" else "golden_r2.npz"))
+    out_path = args.out or str(Path(__file__).resolve().parent / {"r1": "golden.npz", "r2": "golden_r2.npz",
+                                                                    "r3": "golden_r3.npz"}[args.set])
     ss = SwiftShader()
     print("renderer:", ss.renderer)
     store = {"meta_renderer": np.frombuffer(ss.renderer.encode(), dtype=np.uint8),
              "meta_skybox_shape": np.array([SKYBOX_H, SKYBOX_W], dtype=np.int32)}
     names = []
     bound = None
-    for name, kind, cam, params, W, H, tr, extras in (cases() if args.set == "r1" else cases_r2()):
+    for name, kind, cam, params, W, H, tr, extras in {"r1": cases, "r2": cases_r2, "r3": cases_r3}[args.set]():
         if args.only and name != args.only:
             continue
         tex_kind = extras.get("textures", "default")
@@ -508,9 +541,12 @@ def main(argv=None):
             bound = tex_kind
         profile = extras.get("profile", "default")
         scene = scene_for(kind, sizes, mx)
+        rows = extras.get("rows")
         t0 = time.time()
-        img = ss.render(scene, cam, params, W, H, tr, profile=profile)
+        img = ss.render(scene, cam, params, W, H, tr, profile=profile, rows=rows)
         dt = time.time() - t0
+        if rows:
+            store[f"{name}/rows"] = np.array(rows, dtype=np.int32)
         store[f"{name}/rgba8"] = img
         store[f"{name}/scene"] = sc.struct_bytes(scene)
         store[f"{name}/camera"] = sc.struct_bytes(cam)
@@ -519,14 +555,15 @@ def main(argv=None):
         store[f"{name}/test_ray"] = sc.struct_bytes(tr if tr is not None else abi.default_test_ray())
         if tex_kind != "default":
             store[f"{name}/textures"] = np.frombuffer(tex_kind.encode(), dtype=np.uint8)
-        msg = f"{name:22s} {W}x{H} steps={params.max_steps} {dt:6.2f}s"
+        msg = f"{name:22s} {W}x{H}{' rows %d-%d' % rows if rows else ''} steps={params.max_steps} {dt:6.2f}s"
         if extras.get("steps"):
-            st = ss.render(scene, cam, params, W, H, tr, steps_variant=True, profile=profile)
+            st = ss.render(scene, cam, params, W, H, tr, steps_variant=True, profile=profile, rows=rows)
             steps = st[:, :, 0].astype(np.int32) + 256 * st[:, :, 1].astype(np.int32)
             store[f"{name}/steps"] = steps.astype(np.uint16)
             msg += f" mean_steps={steps.mean():.1f}"
         if extras.get("float"):
-            store[f"{name}/rgba32"] = ss.render(scene, cam, params, W, H, tr, float_target=True, profile=profile)
+            store[f"{name}/rgba32"] = ss.render(scene, cam, params, W, H, tr, float_target=True, profile=profile,
+                                                rows=rows)
         names.append(name)
         print(msg, flush=True)
     store["meta_cases"] = np.frombuffer("\n".join(names).encode(), dtype=np.uint8)

@@ -1,0 +1,181 @@
+"""Full-frame, exact parity at every GPU config of BASELINE.json, on the
+bench's own inputs (the reference's textures, the app's default scene and
+camera, src/main.cpp:57-63, 207-268).
+
+tests/golden/make_frame_hashes.py ran the CPU oracle over these frames in the
+build container and committed, per row, sha256 of the RGBA8 bytes and of the
+int32 executed-step counts (tests/golden/frame_hashes.npz). Here the GPU
+renders the same frames - through the paths bench.py uses: batched launches
+with a learned launch order, and config 4 as its eight cost-balanced rank
+shares reassembled by dist.assemble_lists - and every row hash must be equal.
+No tolerance: the arithmetic contract makes the kernel's
+pixels the oracle's bit for bit. Mismatching rows are re-run through the
+oracle for the failure message.
+"""
+import hashlib
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FIXTURE = Path(__file__).resolve().parent / "golden" / "frame_hashes.npz"
+BLOCK_ROWS = 8
+
+
+@pytest.fixture(scope="module")
+def fh():
+    if not FIXTURE.exists():
+        pytest.skip("tests/golden/frame_hashes.npz missing (python tests/golden/make_frame_hashes.py)")
+    with np.load(FIXTURE) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def assets(pkg):
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    A = pkg.assets
+    if not A.available():
+        pytest.skip("assets/textures missing")
+    arr, _, _ = A.texture_array()
+    return {"2k": A.skybox("2k"), "arr": arr}
+
+
+def renderer(pkg, assets, skybox):
+    r = pkg.Renderer(0)
+    r.set_scene(pkg.scenes.scene_default(textured=True))
+    r.set_background(assets[skybox] if skybox in assets else pkg.assets.skybox(skybox))
+    r.set_texture_array(assets["arr"])
+    return r
+
+
+def sha_rows(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a)
+    return np.stack([np.frombuffer(hashlib.sha256(a[k].tobytes()).digest(), dtype=np.uint8)
+                     for k in range(a.shape[0])])
+
+
+def compare(pkg, fh, cfg, rgba8, steps=None, what=""):
+    """Every fixture row of the frame: RGBA8 (and step) hashes equal."""
+    W, H, N = (int(v) for v in fh[f"{cfg}/config"])
+    rows = fh[f"{cfg}/rows"]
+    assert rgba8.shape == (H, W, 4)
+    bad = np.flatnonzero((sha_rows(rgba8[rows]) != fh[f"{cfg}/rgba_sha"]).any(-1))
+    bad_s = np.array([], dtype=np.int64)
+    if steps is not None:
+        bad_s = np.flatnonzero((sha_rows(steps[rows].astype("<i4")) != fh[f"{cfg}/steps_sha"]).any(-1))
+    if len(bad) or len(bad_s):
+        msg = [f"{cfg} {what}: {len(bad)} RGBA8 rows and {len(bad_s)} step rows of {len(rows)} differ"]
+        try:  # diagnostics: the oracle's pixels of the first mismatching rows
+            import srpkg
+
+            oracle = srpkg.load_oracle()
+            sky = bytes(fh[f"{cfg}/skybox"]).decode()
+            A = pkg.assets
+            arr, _, _ = A.texture_array()
+            tex = oracle.TextureSet(A.skybox(sky), arr)
+            params = pkg.abi.default_params(max_steps=N, percent_black=-1.0)
+            for k in list(bad[:3]) + list(bad_s[:2]):
+                y = int(rows[k])
+                rb, _, rs = oracle.render(pkg.scenes.scene_default(textured=True), pkg.abi.default_camera(), params,
+                                          W, H, tex, None, y, y + 1)
+                px = (rb[0] != rgba8[y]).any(-1)
+                msg.append(f"row {y}: {int(px.sum())} px differ (first at x={np.flatnonzero(px)[:5].tolist()})"
+                           + ("" if steps is None else f", {int((rs[0] != steps[y]).sum())} step counts"))
+        except Exception as e:  # noqa: BLE001
+            msg.append(f"(oracle diagnostics failed: {e})")
+        raise AssertionError("\n".join(msg))
+    return len(rows)
+
+
+def frame_digest(rgba8):
+    return hashlib.sha256(np.ascontiguousarray(sha_rows(rgba8)).tobytes()).hexdigest()
+
+
+def test_fixture_covers_the_configs(fh):
+    """configs 2-4 in full; config 5 at least the 512 rows through the hole plus 64 spread"""
+    for cfg, H in (("c2", 360), ("c3", 1080), ("c4", 2160)):
+        assert len(fh[f"{cfg}/rows"]) == H, cfg
+    assert len(fh["c5/rows"]) >= 512 + 60
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3"])
+def test_full_frame_exact(pkg, fh, assets, cfg):
+    """Configs 2 and 3 (the metric): the debug render (steps) and the bench's
+    batched launches (eight static-camera frames, second launch on the
+    learned cost order), every row of every frame."""
+    import torch
+
+    W, H, N = (int(v) for v in fh[f"{cfg}/config"])
+    abi = pkg.abi
+    r = renderer(pkg, assets, "2k")
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    cam = abi.default_camera()
+    _, b, s = r.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    compare(pkg, fh, cfg, b.cpu().numpy(), s.cpu().numpy(), "debug render")
+    B = 8
+    for _ in range(2):
+        out, rows = r.render_blocks_batch([cam] * B, params, W, H, BLOCK_ROWS, 0, 1)
+    torch.cuda.synchronize()
+    assert rows == H
+    frames = out.cpu().numpy()
+    for f in range(B):
+        compare(pkg, fh, cfg, frames[f, :H], None, f"batched frame {f}")
+    if f"{cfg}/frame_sha" in fh:
+        assert frame_digest(frames[B - 1, :H]) == bytes(fh[f"{cfg}/frame_sha"]).hex()
+    r.close()
+
+
+def test_config4_rank_shares_assembled(pkg, fh, assets):
+    """Config 4 (3840x2160, 4000 steps, row-tiled over 8 GPUs): the eight
+    cost-balanced rank shares of bench.py (sr_wave_costs -> dist.block_costs
+    -> balanced_blocks -> sr_render_block_list, two frames per launch)
+    reassembled by dist.assemble_lists, and the step map of the debug render."""
+    import torch
+
+    W, H, N = (int(v) for v in fh["c4/config"])
+    abi, D = pkg.abi, pkg.dist
+    r = renderer(pkg, assets, "2k")
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    cam = abi.default_camera()
+    _, b, s = r.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    compare(pkg, fh, "c4", b.cpu().numpy(), s.cpu().numpy(), "debug render")
+    del b, s
+    world = 8
+    lists = D.balanced_blocks(D.block_costs(r.wave_costs(cam, params, W, H)), world)
+    tiles = []
+    for lst in lists:
+        for _ in range(2):  # the second launch runs the list's learned order
+            t = r.render_block_list([cam, cam], params, W, H, BLOCK_ROWS, lst)
+        tiles.append(t.cpu().numpy())
+    frames = D.assemble_lists(np.stack(tiles), lists, H, BLOCK_ROWS)
+    for f in range(2):
+        compare(pkg, fh, "c4", frames[f], None, f"8 rank shares, frame {f}")
+    r.close()
+
+
+def test_config5_still_8k(pkg, fh, assets):
+    """Config 5 (7680x4320 offline still, 8000 steps, the 8k skybox): every
+    row the fixture holds (the whole frame when make_frame_hashes.py finished
+    it), RGBA8 and step counts, and a second frame through the learned order."""
+    import torch
+
+    W, H, N = (int(v) for v in fh["c5/config"])
+    abi = pkg.abi
+    r = renderer(pkg, assets, bytes(fh["c5/skybox"]).decode())
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    cam = abi.default_camera()
+    _, b, s = r.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    compare(pkg, fh, "c5", b.cpu().numpy(), s.cpu().numpy(), "debug render")
+    del b, s
+    for _ in range(2):
+        out = r.render(cam, params, W, H)
+    torch.cuda.synchronize()
+    compare(pkg, fh, "c5", out.cpu().numpy(), None, "second frame")
+    r.close()

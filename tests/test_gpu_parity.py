@@ -1,21 +1,19 @@
 """HIP kernel (libsr.so, via the C-ABI) vs the CPU oracle.
 
 Contract: both sides evaluate the reference shader's float32
-expressions in the same order with the same rounding, so outputs are expected
-to be bit-identical: float FragColor, RGBA8 pixel and executed step count.
-The only allowed source of difference is the binary64 transcendental
-libraries (glibc on the host vs ocml on the device), which round to the same
-binary32 except when a result falls within one binary64 ulp of a binary32
-rounding boundary; the budget for that is MAX_MISMATCH_FRAC of pixels.
+expressions in the same order with the same rounding, so outputs are
+bit-identical: float FragColor, RGBA8 pixel and executed step count, asserted
+exactly (no pixel may differ). The binary64 transcendentals (glibc on the
+host, ocml on the device) round to the same binary32 on every input these
+tests and the full-frame fixtures (tests/test_gpu_frames.py) reach.
 """
 import numpy as np
 import pytest
 
-from conftest import case_texture_kind, load_case, texture_array_of
+from conftest import case_rows, case_texture_kind, load_case, texture_array_of
 
 pytestmark = pytest.mark.gpu
 
-MAX_MISMATCH_FRAC = 1e-4  # tolerance: <= 0.01% of pixels may differ in any byte
 
 
 @pytest.fixture(scope="module")
@@ -57,8 +55,9 @@ def compare(gpu_out, ora_out, label):
     fbits = (f.view(np.uint32) != rf.view(np.uint32)).any(-1) & ~(np.isnan(f).any(-1) & np.isnan(rf).any(-1))
     msg = (f"{label}: rgba8 differ {px_diff.sum()}/{n}, float-bits differ {fbits.sum()}, "
            f"steps differ {(s != rs).sum()}, max byte diff {np.abs(b.astype(int) - rb.astype(int)).max()}")
-    assert frac <= MAX_MISMATCH_FRAC, msg
-    assert steps_frac <= MAX_MISMATCH_FRAC, msg
+    assert frac == 0, msg
+    assert steps_frac == 0, msg
+    assert fbits.sum() == 0, msg
     return msg
 
 
@@ -69,8 +68,9 @@ def oracle_tex(oracle, textures):
 
 
 def test_golden_cases_bit_exact(pkg, oracle, golden, golden_cases, textures):
-    """Every golden case (golden.npz and golden_r2.npz: the reseed branch,
-    config 2 at full size, the material-flag scene), GPU == oracle."""
+    """Every golden case (golden.npz, golden_r2.npz: the reseed branch,
+    config 2 at full size, the material-flag scene; golden_r3.npz: bands of
+    the headline-size frames), GPU == oracle."""
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
@@ -86,10 +86,11 @@ def test_golden_cases_bit_exact(pkg, oracle, golden, golden_cases, textures):
         otex = oracle.TextureSet(bg, arr)
         for name in names:
             scene, cam, params, tr, w, h = load_case(pkg, golden, name)
-            g = gpu_debug(r, scene, cam, params, w, h, tr)
-            o = oracle.render(scene, cam, params, w, h, otex, tr)
+            y0, y1 = case_rows(golden, name, h)
+            g = gpu_debug(r, scene, cam, params, w, h, tr, y0, y1)
+            o = oracle.render(scene, cam, params, w, h, otex, tr, y0, y1)
             print(compare(g, o, name))
-            if name.startswith("reseed") or name.startswith("config2"):
+            if name.startswith(("reseed", "config2", "band")):
                 assert (g[2] != o[2]).sum() == 0, f"{name}: step counts differ"
         r.close()
 
@@ -354,78 +355,22 @@ def test_rows_and_blocks_assemble_full_frame(pkg, gpu):
         assert np.array_equal(frame, full), nranks
 
 
-def test_headline_frame_sampled_rows(pkg, gpu, oracle, oracle_tex):
-    """1920x1080 / 2000 steps (the bench workload): 24 rows spread over the
-    frame bit-compared with the oracle, and run-to-run determinism."""
+def test_headline_frame_deterministic(pkg, gpu):
+    """The metric's frame with the procedural golden textures: two launches
+    byte-identical and the mean step count of SURVEY §8d (full-frame parity on
+    the bench's own inputs is tests/test_gpu_frames.py)."""
     import torch
 
     sc, abi = pkg.scenes, pkg.abi
-    scene = sc.scene_default(textured=True)
-    cam = abi.default_camera()
+    gpu.set_scene(sc.scene_default(textured=True))
+    gpu.set_test_ray(abi.default_test_ray())
     params = abi.default_params(max_steps=2000, percent_black=-1.0)
-    W, H = 1920, 1080
-    gpu.set_scene(scene)
-    gpu.set_test_ray(abi.default_test_ray())
-    f, b, s = gpu.render_debug(cam, params, W, H)
-    b2 = gpu.render(cam, params, W, H)
+    _, b, s = gpu.render_debug(abi.default_camera(), params, 1920, 1080)
+    b2 = gpu.render(abi.default_camera(), params, 1920, 1080)
     torch.cuda.synchronize()
-    b, s, b2 = b.cpu().numpy(), s.cpu().numpy(), b2.cpu().numpy()
-    assert np.array_equal(b, b2)
-    rows = np.linspace(0, H - 1, 24).astype(int)
-    for y in rows:
-        rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
-        assert (rb[0] != b[y]).any(-1).mean() <= 1e-3, f"row {y}"
-        assert (rs[0] != s[y]).mean() <= 1e-3, f"row {y}"
+    assert torch.equal(b, b2)
     # SURVEY §8d: mean executed steps per pixel at N=2000 ~ 0.206 N
-    assert 380 < s.mean() < 440, s.mean()
-
-
-def test_config4_rank_share_4k(pkg, gpu, oracle, oracle_tex):
-    """BASELINE config 4 (3840x2160, 4000 steps, row-tiled over 8 GPUs): rank
-    3's block-cyclic share rendered through sr_render_blocks, the multi-GPU
-    data path of bench.py, and three of its rows bit-compared with the oracle."""
-    import torch
-
-    sc, abi, D = pkg.scenes, pkg.abi, pkg.dist
-    scene = sc.scene_default(textured=True)
-    cam = abi.default_camera()
-    params = abi.default_params(max_steps=4000, percent_black=-1.0)
-    W, H, br, world, rank = 3840, 2160, 8, 8, 3
-    gpu.set_scene(scene)
-    gpu.set_test_ray(abi.default_test_ray())
-    tile, nrows = gpu.render_blocks(cam, params, W, H, br, rank, world)
-    torch.cuda.synchronize()
-    tile = tile.cpu().numpy()
-    rows = D.rows_of(rank, world, H, br)
-    assert nrows == len(rows) and tile.shape[0] >= len(rows)
-    for k in (0, len(rows) // 2 + 3, len(rows) - 1):  # edge, through the photon ring, edge
-        y = rows[k]
-        rb, _, _ = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
-        assert (rb[0] != tile[k]).any(-1).mean() <= 1e-3, f"row {y}"
-
-
-def test_config5_band_8k(pkg, gpu, oracle, oracle_tex):
-    """BASELINE config 5 (7680x4320 offline still, 8000 steps): a 16-row band
-    through the black hole rendered alone, two rows bit-compared with the
-    oracle (executed step counts too)."""
-    import torch
-
-    sc, abi = pkg.scenes, pkg.abi
-    scene = sc.scene_default(textured=True)
-    cam = abi.default_camera()
-    params = abi.default_params(max_steps=8000, percent_black=-1.0)
-    W, H = 7680, 4320
-    y0 = H // 2 - 8
-    gpu.set_scene(scene)
-    gpu.set_test_ray(abi.default_test_ray())
-    _, b, s = gpu.render_debug(cam, params, W, H, y0, y0 + 16)
-    torch.cuda.synchronize()
-    b, s = b.cpu().numpy(), s.cpu().numpy()
-    for k in (3, 12):
-        y = y0 + k
-        rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, y, y + 1)
-        assert (rb[0] != b[k]).any(-1).mean() <= 1e-3, f"row {y}"
-        assert (rs[0] != s[k]).mean() <= 1e-3, f"row {y}"
+    assert 380 < float(s.float().mean()) < 440
 
 
 @pytest.mark.parametrize("seed", range(8))
@@ -550,7 +495,7 @@ def test_reseed_headline_rows(pkg, gpu, oracle, oracle_tex, name, pos, fov, u_f)
     rows = sorted(set(rows.tolist()) | set(int(v) for v in np.argsort(s.max(axis=1))[-4:]))
     for y in rows:
         rb, _, rs = oracle.render(scene, cam, params, W, H, oracle_tex, None, int(y), int(y) + 1)
-        assert (rb[0] != b[y]).any(-1).mean() <= 1e-3, f"{name}: row {y}"
+        assert not (rb[0] != b[y]).any(), f"{name}: row {y}"
         assert (rs[0] != s[y]).sum() == 0, f"{name}: row {y} step counts"
 
 
@@ -601,3 +546,62 @@ def test_presentation_png_of_a_gpu_frame(pkg, gpu, tmp_path):
     got = np.asarray(PIL.open(path).convert("RGBA"))
     assert got.shape == (113, 200, 4)
     assert np.array_equal(got, frame[::-1])
+
+
+def test_two_contexts_alternating_shapes_in_flight(pkg, textures):
+    """Render paths allocate in stream order (no device-wide synchronisation):
+    two contexts on two streams with frames in flight, cycling through more
+    frame shapes, step counts and block lists than a context's caches hold
+    (LRU eviction, stream-ordered frees after the in-flight frames). Every
+    frame equals, byte for byte, a fresh context's render of it."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    bg, arr = textures
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+
+    def make():
+        r = pkg.Renderer(0)
+        r.set_scene(scene)
+        r.set_background(bg)
+        r.set_texture_array(arr)
+        return r
+
+    shapes = [(160, 90, 300), (200, 113, 500), (96, 54, 800), (320, 180, 400), (128, 72, 300), (64, 36, 200),
+              (256, 144, 350), (144, 81, 450), (176, 99, 250), (112, 63, 600), (208, 117, 320)]
+    lists = [[5, 0, 2, -1], [1, 3], [4, -1, 0], [2], [0, 1, 2, 3, 4], [3, -1], [4, 2], [1], [0, 4], [2, 3, 1],
+             [5, 4, 3]]
+    lw, lh, ln = 160, 48, 400
+    ref = {}
+    r0 = make()
+    for W, H, N in shapes:
+        ref[(W, H, N)] = r0.render(cam, abi.default_params(max_steps=N, percent_black=-1.0), W, H).cpu().numpy()
+    full = r0.render(cam, abi.default_params(max_steps=ln, percent_black=-1.0), lw, lh).cpu().numpy()
+    r0.close()
+    ctxs, streams = [make(), make()], [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for rep in range(3):
+        for i, (W, H, N) in enumerate(shapes):
+            k = (i + rep) % 2
+            with torch.cuda.stream(streams[k]):
+                out = ctxs[k].render(cam, abi.default_params(max_steps=N, percent_black=-1.0), W, H, stream=streams[k])
+            got.append(((W, H, N), out, streams[k]))
+        for i, blocks in enumerate(lists):
+            k = i % 2
+            with torch.cuda.stream(streams[k]):
+                out = ctxs[k].render_block_list([cam], abi.default_params(max_steps=ln, percent_black=-1.0), lw, lh,
+                                                8, blocks, stream=streams[k])
+            got.append((tuple(blocks), out, streams[k]))
+    torch.cuda.synchronize()
+    for key, out, _ in got:
+        o = out.cpu().numpy()
+        if key in ref:
+            assert np.array_equal(o, ref[key]), key
+        else:
+            for s_, b in enumerate(key):
+                if b >= 0:
+                    n = min(8, lh - b * 8)
+                    assert np.array_equal(o[0, s_ * 8:s_ * 8 + n], full[b * 8:b * 8 + n]), (key, b)
+    for c in ctxs:
+        c.close()

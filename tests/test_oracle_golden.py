@@ -4,14 +4,25 @@ SwiftShader 4.1 (tests/golden/make_golden.py).
 
 Tolerance budget. SwiftShader's texture filter, sin/atan/asin
 and interpolation of `uv` are one valid GL implementation, not bit-defined:
-  - untextured scenes:   >= 99.9 % of pixels within 2/255 per channel, at
-                          most 0.05 % beyond 4/255 (SURVEY §7 hard part 1:
-                          rays that orbit the photon ring for hundreds of
-                          steps leave in a direction that differs in the last
-                          bits and may cross a skybox checker edge; seen only
-                          in the far-camera goldens, 1-4 pixels, equal step
-                          counts), executed step counts equal on >= 99.9 % of
-                          pixels;
+  - untextured scenes:   >= 99.9 % of pixels within 2/255 per channel and
+                          every pixel within 4/255; the far-camera reseed
+                          goldens only: at most 0.05 % beyond 4/255 (SURVEY
+                          §7 hard part 1: rays that orbit the photon ring for
+                          hundreds of steps leave in a direction that differs
+                          in the last bits and may cross a skybox checker
+                          edge; 1-4 pixels, equal step counts); executed step
+                          counts equal on >= 99.9 % of pixels. The
+                          headline-size bands (golden_r3.npz) are photon-ring
+                          rays of up to 1,900 (4,000) steps and take that
+                          allowance too: one pixel of 30,720 in rows 704-719,
+                          5/255 after 1,237 equal steps; step counts equal on
+                          99.97 %. The
+                          material-flag goldens (translucent textured
+                          surfaces, normal maps) take the same 0.05 %
+                          allowance: a ray through several translucent
+                          surfaces sums several of SwiftShader's fixed-point
+                          filter results (one pixel of features_low, 5/255,
+                          equal step counts);
   - textured scenes:     SwiftShader samples RGBA8 in 16-bit fixed point, so an
                           opaque texel reads alpha 65527..65531/65535 < 1 and
                           the ray does not stop at textured objects
@@ -27,7 +38,7 @@ and interpolation of `uv` are one valid GL implementation, not bit-defined:
 import numpy as np
 import pytest
 
-from conftest import case_texture_kind, load_case, texture_array_of
+from conftest import case_rows, case_texture_kind, load_case, texture_array_of
 
 UNTEXTURED = ["bh_default", "scene_untex", "mode_half_width", "mode_half_height", "crosshair", "steps_100",
               "test_ray"] + [f"rand_{i}" for i in range(1, 9)]
@@ -40,6 +51,12 @@ TEXTURED = ["scene_tex", "scene_tex_weighted", "scene_tex_2000", "mode_flat"]
 RESEED = ["reseed_r120", "reseed_r300", "reseed_side", "reseed_uf01", "reseed_uf005_far"]
 FEATURES = ["features_default", "features_oblique", "features_low", "features_below", "features_flat"]
 R2_BUDGET = RESEED + ["config2_640x360"] + FEATURES
+# golden_r3.npz: 16-row bands of the headline frame (1920x1080 / 2000 steps:
+# rows 704-719, the photon-ring waves of the critical path, and 536-551,
+# through the black hole) and of config 4 (3840x2160 / 4000 steps), rendered
+# at full frame size under a scissor rectangle
+BANDS_UNTEX = ["band1080_704_untex", "band1080_536_untex", "band2160_1408_untex"]
+BANDS_TEX = ["band1080_704_tex", "band1080_536_tex"]
 
 
 @pytest.fixture(scope="module")
@@ -49,11 +66,16 @@ def tex(oracle, textures):
 
 
 def run(pkg, oracle, golden, tex, name):
+    if name + "/scene" not in golden:
+        pytest.skip(f"{name}: golden missing (python tests/golden/make_golden.py --set r3)")
     scene, cam, params, tr, w, h = load_case(pkg, golden, name)
     kind = case_texture_kind(golden, name)
     if kind != "default":
         tex = oracle.TextureSet(tex.bg, texture_array_of(pkg, kind))
-    rgba8, rgba32, steps = oracle.render(scene, cam, params, w, h, tex, tr)
+    if name + "/rgba8" not in golden:
+        pytest.skip(f"{name}: golden missing (python tests/golden/make_golden.py --set r3)")
+    y0, y1 = case_rows(golden, name, h)
+    rgba8, rgba32, steps = oracle.render(scene, cam, params, w, h, tex, tr, y0, y1)
     return rgba8, rgba32, steps, golden[name + "/rgba8"]
 
 
@@ -74,12 +96,15 @@ def test_reseed_goldens_take_the_branch(pkg, golden):
         assert r > 1.0 / params.u_f, (name, r, params.u_f)
 
 
-@pytest.mark.parametrize("name", UNTEXTURED + R2_BUDGET)
+@pytest.mark.parametrize("name", UNTEXTURED + R2_BUDGET + BANDS_UNTEX)
 def test_untextured_within_budget(pkg, oracle, golden, tex, name):
     rgba8, _, steps, ref = run(pkg, oracle, golden, tex, name)
     d = np.abs(rgba8.astype(int) - ref.astype(int)).max(-1)
     assert np.mean(d <= 2) >= 0.999, (name, np.mean(d <= 2))
-    assert np.mean(d > 4) <= 5e-4, (name, int((d > 4).sum()), d.max())
+    if name in RESEED + FEATURES + BANDS_UNTEX:  # ring rays, far cameras, stacked translucent lookups (docstring)
+        assert np.mean(d > 4) <= 5e-4, (name, int((d > 4).sum()), d.max())
+    else:
+        assert d.max() <= 4, (name, int((d > 4).sum()), d.max())
     if name + "/steps" in golden:
         assert np.mean(golden[name + "/steps"].astype(int) == steps) >= 0.999
 
@@ -93,10 +118,13 @@ def test_float_fragcolor(pkg, oracle, golden, tex, name):
     ref = golden[name + "/rgba32"]
     d = np.abs(rgba32 - ref)
     assert np.median(d) < 2e-4
-    assert np.mean(d.max(-1) >= 0.02) <= 5e-4, (name, int((d.max(-1) >= 0.02).sum()), d.max())
+    if name in RESEED + FEATURES:
+        assert np.mean(d.max(-1) >= 0.02) <= 5e-4, (name, int((d.max(-1) >= 0.02).sum()), d.max())
+    else:
+        assert d.max() < 0.02, (name, int((d.max(-1) >= 0.02).sum()), d.max())
 
 
-@pytest.mark.parametrize("name", TEXTURED)
+@pytest.mark.parametrize("name", TEXTURED + BANDS_TEX)
 def test_textured_pinned_where_alpha_semantics_agree(pkg, oracle, golden, tex, name):
     rgba8, _, steps, ref = run(pkg, oracle, golden, tex, name)
     d = np.abs(rgba8.astype(int) - ref.astype(int)).max(-1)
@@ -104,9 +132,14 @@ def test_textured_pinned_where_alpha_semantics_agree(pkg, oracle, golden, tex, n
         same = golden[name + "/steps"].astype(int) == steps
     else:  # the scene_tex step map is the same for every frame of that camera at this size
         same = d <= 4
-    assert same.mean() >= 0.75, same.mean()
+    # the headline bands cross the textured box / sphere / disk more often than
+    # the small frames: more rays SwiftShader lets through (alpha < 1)
+    assert same.mean() >= (0.6 if name in BANDS_TEX else 0.75), same.mean()
     assert np.mean(d[same] <= 2) >= 0.999
-    assert d[same].max() <= 4
+    if name in BANDS_TEX:  # photon-ring rays of the untextured allowance
+        assert np.mean(d[same] > 4) <= 5e-4, (name, int((d[same] > 4).sum()))
+    else:
+        assert d[same].max() <= 4
 
 
 def test_noise_mask_statistics(pkg, oracle, golden, tex):

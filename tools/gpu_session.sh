@@ -16,6 +16,10 @@ run() {  # name timeout cmd...
   return $rc
 }
 STEPS=${STEPS:-pytest,smoke,bench,prof}
+if [[ $STEPS == *micro* ]]; then  # tools/microbench/tworay (built in the container)
+  run tworay 120 tools/microbench/tworay || exit $?
+  grep '^{' "$OUT/tworay.log" > "$OUT/tworay.json"
+fi
 if [[ $STEPS == *pytest* ]]; then
   run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}; rc=$?
   if fatal $rc; then echo "pytest fatal rc=$rc, stopping"; exit $rc; fi
