@@ -1,0 +1,410 @@
+// sr_multi_gpu.cpp — the reference's frame loop (src/main.cpp:303-432: one
+// full-screen draw per frame, src/main.cpp:318-319) on the GPUs of one node,
+// written against the C-ABI of include/sr/sr.h the way a C++ host would
+// drive it: RCCL over xGMI, no Python.
+//
+//   per node    sr_wave_costs (one frame, root GPU) -> sr_block_costs ->
+//               sr_balanced_blocks: equal-length lists of 8-row blocks of
+//               about equal cost, one per rank
+//   per launch  every GPU: sr_render_block_list (B frames, its list) on its
+//               stream; ncclGather of the equal-size tiles to the root;
+//               root: sr_assemble_blocks (device kernel) -> B frames
+//
+// Two ways to run it:
+//   one process, N GPUs     ./sr_multi_gpu --gpus N ...        (ncclCommInitAll)
+//   one process per GPU     RANK=r WORLD_SIZE=N LOCAL_RANK=r ./sr_multi_gpu --id-file F ...
+//                           (ncclCommInitRank; rank 0 writes the unique id to F,
+//                           prices the blocks and ncclBroadcasts the lists)
+// Textures: raw files (--skybox PATH:W:H with RGB8 rows bottom-up, --array
+// PATH:W:H:L with RGBA8 layers, as sr_set_background / sr_set_texture_array
+// take them) or procedural stand-ins. --out-raw writes the last frame (RGBA8,
+// rows bottom-up) for checking; one JSON line goes to stdout.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sr/sr.h"
+
+namespace {
+
+#define CHECK_SR(x)                                                                           \
+    do {                                                                                      \
+        const int rc_ = (x);                                                                  \
+        if (rc_ != SR_OK) {                                                                   \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, sr_status_string(rc_)); \
+            std::exit(2);                                                                     \
+        }                                                                                     \
+    } while (0)
+#define CHECK_HIP(x)                                                                          \
+    do {                                                                                      \
+        const hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) {                                                               \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(2);                                                                     \
+        }                                                                                     \
+    } while (0)
+#define CHECK_NCCL(x)                                                                         \
+    do {                                                                                      \
+        const ncclResult_t r_ = (x);                                                          \
+        if (r_ != ncclSuccess) {                                                              \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, ncclGetErrorString(r_)); \
+            std::exit(2);                                                                     \
+        }                                                                                     \
+    } while (0)
+
+constexpr int kBlockRows = 8;  // one 8x8 wave tile tall
+
+struct Args {
+    int gpus = 1, width = 1920, height = 1080, max_steps = 2000, frames = 16, batch = 8, warmup = 8;
+    bool flyby = false;
+    std::string skybox, array, out_raw, id_file;
+};
+
+void usage() {
+    std::printf(
+        "sr_multi_gpu [--gpus N] [--width W] [--height H] [--max-steps N] [--frames K] [--batch B]\n"
+        "             [--warmup W] [--flyby] [--skybox PATH:W:H] [--array PATH:W:H:L] [--out-raw PATH]\n"
+        "             [--id-file PATH]   (one process per GPU: RANK / WORLD_SIZE / LOCAL_RANK from the env)\n");
+}
+
+Args parse(int argc, char** argv) {
+    Args a;
+    for (int i = 1; i < argc; i++) {
+        const std::string k = argv[i];
+        auto next = [&]() -> const char* {
+            if (i + 1 >= argc) {
+                usage();
+                std::exit(1);
+            }
+            return argv[++i];
+        };
+        if (k == "--help" || k == "-h") {
+            usage();
+            std::exit(0);
+        } else if (k == "--gpus") a.gpus = std::atoi(next());
+        else if (k == "--width") a.width = std::atoi(next());
+        else if (k == "--height") a.height = std::atoi(next());
+        else if (k == "--max-steps") a.max_steps = std::atoi(next());
+        else if (k == "--frames") a.frames = std::atoi(next());
+        else if (k == "--batch") a.batch = std::atoi(next());
+        else if (k == "--warmup") a.warmup = std::atoi(next());
+        else if (k == "--flyby") a.flyby = true;
+        else if (k == "--skybox") a.skybox = next();
+        else if (k == "--array") a.array = next();
+        else if (k == "--out-raw") a.out_raw = next();
+        else if (k == "--id-file") a.id_file = next();
+        else {
+            usage();
+            std::exit(1);
+        }
+    }
+    return a;
+}
+
+std::vector<std::string> split(const std::string& s) {
+    std::vector<std::string> out;
+    size_t p = 0;
+    for (;;) {
+        const size_t q = s.find(':', p);
+        out.push_back(s.substr(p, q == std::string::npos ? std::string::npos : q - p));
+        if (q == std::string::npos) return out;
+        p = q + 1;
+    }
+}
+
+std::vector<uint8_t> read_file(const std::string& path, size_t bytes) {
+    std::ifstream f(path, std::ios::binary);
+    std::vector<uint8_t> v(bytes);
+    if (!f.read(reinterpret_cast<char*>(v.data()), (std::streamsize)bytes)) {
+        std::fprintf(stderr, "cannot read %zu bytes from %s\n", bytes, path.c_str());
+        std::exit(1);
+    }
+    return v;
+}
+
+// One GPU's share of the node.
+struct Device {
+    int dev = 0;
+    sr_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;
+    uint8_t* tile = nullptr;     // B frames of per * kBlockRows rows
+    ncclComm_t comm = nullptr;
+    hipEvent_t r0 = nullptr, r1 = nullptr, g1 = nullptr;  // render start / end, gather end (timed launches)
+    double render_ms = 0.0, gather_ms = 0.0;
+};
+
+void setup_device(Device& d, const Args& a, const sr_scene& scene, size_t tile_bytes) {
+    CHECK_HIP(hipSetDevice(d.dev));
+    CHECK_SR(sr_create(&d.ctx, d.dev));
+    CHECK_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    CHECK_HIP(hipMalloc(&d.tile, tile_bytes));
+    CHECK_HIP(hipEventCreate(&d.r0));
+    CHECK_HIP(hipEventCreate(&d.r1));
+    CHECK_HIP(hipEventCreate(&d.g1));
+    CHECK_SR(sr_set_scene(d.ctx, &scene));
+    if (!a.skybox.empty()) {
+        const auto f = split(a.skybox);
+        const int w = std::atoi(f.at(1).c_str()), h = std::atoi(f.at(2).c_str());
+        const auto px = read_file(f[0], (size_t)w * h * 3);
+        CHECK_SR(sr_set_background(d.ctx, px.data(), w, h, 3));
+    } else {  // procedural stand-in: an 8x8-cell checker, 2048x1024 RGB
+        const int w = 2048, h = 1024;
+        std::vector<uint8_t> px((size_t)w * h * 3);
+        for (int y = 0; y < h; y++)
+            for (int x = 0; x < w; x++) {
+                uint8_t* p = &px[((size_t)y * w + x) * 3];
+                const bool c = ((x >> 7) + (y >> 7)) & 1;
+                p[0] = (uint8_t)(c ? 200 : 30);
+                p[1] = (uint8_t)(x * 255 / w);
+                p[2] = (uint8_t)(y * 255 / h);
+            }
+        CHECK_SR(sr_set_background(d.ctx, px.data(), w, h, 3));
+    }
+    if (!a.array.empty()) {
+        const auto f = split(a.array);
+        const int w = std::atoi(f.at(1).c_str()), h = std::atoi(f.at(2).c_str()), l = std::atoi(f.at(3).c_str());
+        const auto px = read_file(f[0], (size_t)w * h * l * 4);
+        CHECK_SR(sr_set_texture_array(d.ctx, px.data(), w, h, l, 4));
+    } else {  // opaque stand-in layers of the reference array's size (1601x1201, two layers)
+        const int w = 1601, h = 1201, l = 2;
+        std::vector<uint8_t> px((size_t)w * h * l * 4);
+        for (size_t i = 0; i < (size_t)w * h * l; i++) {
+            px[4 * i] = (uint8_t)(i * 7);
+            px[4 * i + 1] = (uint8_t)(i * 13);
+            px[4 * i + 2] = (uint8_t)(i * 29);
+            px[4 * i + 3] = 255;
+        }
+        CHECK_SR(sr_set_texture_array(d.ctx, px.data(), w, h, l, 4));
+    }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    const Args a = parse(argc, argv);
+    const char* ws = std::getenv("WORLD_SIZE");
+    const bool per_process = ws && std::atoi(ws) > 1;
+    const int world = per_process ? std::atoi(ws) : a.gpus;
+    const int rank = per_process ? std::atoi(std::getenv("RANK") ? std::getenv("RANK") : "0") : 0;
+    const int local = per_process ? std::atoi(std::getenv("LOCAL_RANK") ? std::getenv("LOCAL_RANK") : "0") : 0;
+    int ndev = 0;
+    CHECK_HIP(hipGetDeviceCount(&ndev));
+    if (!per_process && (world < 1 || world > ndev)) {
+        std::fprintf(stderr, "--gpus %d: %d device(s) visible\n", world, ndev);
+        return 1;
+    }
+    if (a.batch < 1 || a.batch > 32 || a.frames < 1) {
+        std::fprintf(stderr, "--batch must be 1..32, --frames >= 1\n");
+        return 1;
+    }
+    const int W = a.width, H = a.height, B = a.batch;
+    const int nb = (H + kBlockRows - 1) / kBlockRows, nc = (W + 7) / 8;
+    const int per = (nb + world - 1) / world;
+    const size_t row_bytes = (size_t)W * 4, tile_frame = (size_t)per * kBlockRows * row_bytes;
+    const size_t tile_bytes = tile_frame * B;
+
+    sr_scene scene;
+    sr_default_scene(&scene);  // src/main.cpp:222-268
+    if (!a.array.empty()) {
+        const auto f = split(a.array);
+        scene.max_texture_size[0] = (float)std::atoi(f.at(1).c_str());
+        scene.max_texture_size[1] = (float)std::atoi(f.at(2).c_str());
+    }
+    sr_params params;
+    sr_params_default(&params);
+    params.max_steps = a.max_steps;
+    params.percent_black = -1.0f;  // the benchmark's setting
+
+    // ---- devices and communicators ----
+    std::vector<Device> devs(per_process ? 1 : world);
+    if (per_process) {
+        devs[0].dev = local % ndev;
+        ncclUniqueId id;
+        const std::string path = a.id_file.empty() ? std::string("/tmp/sr_multi_gpu.ncclid") : a.id_file;
+        if (rank == 0) {
+            CHECK_NCCL(ncclGetUniqueId(&id));
+            const std::string tmp = path + ".tmp";
+            std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(&id), sizeof id);
+            std::rename(tmp.c_str(), path.c_str());
+        } else {
+            for (int t = 0;; t++) {
+                std::ifstream f(path, std::ios::binary);
+                if (f.read(reinterpret_cast<char*>(&id), sizeof id)) break;
+                if (t > 6000) {
+                    std::fprintf(stderr, "rank %d: no NCCL id in %s\n", rank, path.c_str());
+                    return 1;
+                }
+                std::this_thread::sleep_for(std::chrono::milliseconds(10));
+            }
+        }
+        CHECK_HIP(hipSetDevice(devs[0].dev));
+        CHECK_NCCL(ncclCommInitRank(&devs[0].comm, world, id, rank));
+    } else {
+        std::vector<ncclComm_t> comms(world);
+        std::vector<int> ids(world);
+        for (int d = 0; d < world; d++) ids[d] = devs[d].dev = d;
+        CHECK_NCCL(ncclCommInitAll(comms.data(), world, ids.data()));
+        for (int d = 0; d < world; d++) devs[d].comm = comms[d];
+    }
+    for (auto& d : devs) setup_device(d, a, scene, tile_bytes);
+    const bool root = rank == 0;  // devs[0] is the root GPU in the one-process mode
+    Device& r0 = devs[0];
+
+    // cameras: the app's default, or its H-key flyby (src/main.cpp:404-410)
+    const int n_total = a.warmup + a.frames;
+    std::vector<sr_camera> cams(n_total);
+    for (int f = 0; f < n_total; f++) {
+        sr_default_camera(&cams[f]);
+        if (a.flyby) CHECK_SR(sr_camera_hyperbolic_trajectory(&cams[f], 30.0f, 10.0f, (f + 0.5f) / n_total));
+    }
+
+    // ---- pricing on the root GPU, lists to every rank ----
+    std::vector<int> lists((size_t)world * per, -1);
+    double max_over_mean = 1.0;
+    {
+        int32_t* d_costs = nullptr;
+        if (root) {
+            CHECK_HIP(hipSetDevice(r0.dev));
+            CHECK_HIP(hipMalloc(&d_costs, (size_t)nb * nc * 2 * sizeof(int32_t)));
+            CHECK_SR(sr_wave_costs(r0.ctx, &cams[0], &params, W, H, d_costs, r0.stream));
+            std::vector<int32_t> wc((size_t)nb * nc * 2);
+            CHECK_HIP(hipMemcpyAsync(wc.data(), d_costs, wc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, r0.stream));
+            CHECK_HIP(hipStreamSynchronize(r0.stream));
+            CHECK_HIP(hipFree(d_costs));
+            std::vector<double> cost(nb);
+            CHECK_SR(sr_block_costs(wc.data(), nb, nc, 8.0, cost.data()));
+            int got = 0;
+            CHECK_SR(sr_balanced_blocks(cost.data(), nb, world, lists.data(), (int)lists.size(), &got));
+            double mx = 0.0, sum = 0.0;
+            for (int r = 0; r < world; r++) {
+                double l = 0.0;
+                for (int s = 0; s < per; s++)
+                    if (lists[(size_t)r * per + s] >= 0) l += cost[lists[(size_t)r * per + s]];
+                mx = std::max(mx, l);
+                sum += l;
+            }
+            max_over_mean = sum > 0.0 ? mx / (sum / world) : 1.0;
+        }
+        if (per_process) {  // the root's lists to every rank (one broadcast, int32)
+            int* d_l = nullptr;
+            CHECK_HIP(hipSetDevice(r0.dev));
+            CHECK_HIP(hipMalloc(&d_l, lists.size() * sizeof(int)));
+            CHECK_HIP(hipMemcpyAsync(d_l, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, r0.stream));
+            CHECK_NCCL(ncclBroadcast(d_l, d_l, lists.size(), ncclInt32, 0, r0.comm, r0.stream));
+            CHECK_HIP(hipMemcpyAsync(lists.data(), d_l, lists.size() * sizeof(int), hipMemcpyDeviceToHost, r0.stream));
+            CHECK_HIP(hipStreamSynchronize(r0.stream));
+            CHECK_HIP(hipFree(d_l));
+        }
+    }
+
+    // root buffers: the gathered tiles, the lists on the device, the frames
+    uint8_t *stacked = nullptr, *frames = nullptr;
+    int* d_lists = nullptr;
+    if (root) {
+        CHECK_HIP(hipSetDevice(r0.dev));
+        CHECK_HIP(hipMalloc(&stacked, tile_bytes * world));
+        CHECK_HIP(hipMalloc(&frames, (size_t)B * H * row_bytes));
+        CHECK_HIP(hipMalloc(&d_lists, lists.size() * sizeof(int)));
+        CHECK_HIP(hipMemcpy(d_lists, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice));
+    }
+
+    // one launch: frames [first, first + n) on every GPU, gathered, reassembled
+    auto launch = [&](int first, int n, bool timed) {
+        for (size_t k = 0; k < devs.size(); k++) {
+            Device& d = devs[k];
+            const int r = per_process ? rank : (int)k;
+            CHECK_HIP(hipSetDevice(d.dev));
+            if (timed) CHECK_HIP(hipEventRecord(d.r0, d.stream));
+            CHECK_SR(sr_render_block_list(d.ctx, &cams[first], n, &params, W, H, kBlockRows, &lists[(size_t)r * per],
+                                          per, d.tile, row_bytes, tile_frame, d.stream));
+            if (timed) CHECK_HIP(hipEventRecord(d.r1, d.stream));
+        }
+        // equal-size tiles to the root over xGMI (each peer on its own link)
+        CHECK_NCCL(ncclGroupStart());
+        for (size_t k = 0; k < devs.size(); k++) {
+            Device& d = devs[k];
+            const bool is_root = per_process ? root : k == 0;
+            CHECK_NCCL(ncclGather(d.tile, is_root ? stacked : nullptr, tile_bytes, ncclUint8, 0, d.comm, d.stream));
+        }
+        CHECK_NCCL(ncclGroupEnd());
+        for (auto& d : devs)
+            if (timed) {
+                CHECK_HIP(hipSetDevice(d.dev));
+                CHECK_HIP(hipEventRecord(d.g1, d.stream));
+            }
+        if (root) {
+            CHECK_HIP(hipSetDevice(r0.dev));
+            CHECK_SR(sr_assemble_blocks(stacked, tile_bytes, tile_frame, d_lists, world, per, H, kBlockRows, row_bytes,
+                                        frames, (size_t)H * row_bytes, n, 1, r0.stream));
+        }
+        if (timed) {  // per-launch device times (the launches of a run are sequential per GPU)
+            for (auto& d : devs) {
+                CHECK_HIP(hipEventSynchronize(d.g1));
+                float rm = 0.f, gm = 0.f;
+                CHECK_HIP(hipEventElapsedTime(&rm, d.r0, d.r1));
+                CHECK_HIP(hipEventElapsedTime(&gm, d.r1, d.g1));
+                d.render_ms += rm;
+                d.gather_ms += gm;
+            }
+        }
+    };
+    auto sync_all = [&]() {
+        for (auto& d : devs) {
+            CHECK_HIP(hipSetDevice(d.dev));
+            CHECK_HIP(hipStreamSynchronize(d.stream));
+        }
+    };
+    for (int f = 0; f < a.warmup; f += B) launch(f, std::min(B, a.warmup - f), false);
+    sync_all();
+    const auto t0 = std::chrono::steady_clock::now();
+    int last_n = 0;
+    for (int f = 0; f < a.frames; f += B) {
+        last_n = std::min(B, a.frames - f);
+        launch(a.warmup + f, last_n, true);
+    }
+    sync_all();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+
+    if (root && !a.out_raw.empty()) {  // the run's last frame
+        std::vector<uint8_t> h((size_t)H * row_bytes);
+        CHECK_HIP(hipSetDevice(r0.dev));
+        CHECK_HIP(hipMemcpy(h.data(), frames + (size_t)(last_n - 1) * H * row_bytes, h.size(), hipMemcpyDeviceToHost));
+        std::ofstream(a.out_raw, std::ios::binary).write(reinterpret_cast<const char*>(h.data()), (std::streamsize)h.size());
+    }
+    if (root) {
+        std::printf("{\"tool\": \"sr_multi_gpu\", \"mode\": \"%s\", \"world_size\": %d, \"width\": %d, \"height\": %d, "
+                    "\"max_steps\": %d, \"frames\": %d, \"frames_per_launch\": %d, \"camera\": \"%s\", "
+                    "\"value\": %.3f, \"unit\": \"Mpixels/s\", \"ms_per_frame\": %.4f, \"balance_max_over_mean\": %.4f, "
+                    "\"collective\": \"ncclGather of equal-size tiles\", \"ranks\": [",
+                    per_process ? "process per GPU (ncclCommInitRank)" : "one process (ncclCommInitAll)", world, W, H,
+                    a.max_steps, a.frames, B, a.flyby ? "flyby" : "static", (double)W * H * a.frames / sec / 1e6,
+                    sec * 1e3 / a.frames, max_over_mean);
+        for (size_t k = 0; k < devs.size(); k++)
+            std::printf("%s{\"device\": %d, \"render_ms_per_frame\": %.4f, \"gather_ms_per_frame\": %.4f}",
+                        k ? ", " : "", devs[k].dev, devs[k].render_ms / a.frames, devs[k].gather_ms / a.frames);
+        std::printf("]}\n");
+    }
+    for (auto& d : devs) {
+        CHECK_HIP(hipSetDevice(d.dev));
+        sr_destroy(d.ctx);
+        (void)hipFree(d.tile);
+        (void)hipStreamDestroy(d.stream);
+        (void)ncclCommDestroy(d.comm);
+    }
+    if (root) {
+        CHECK_HIP(hipSetDevice(r0.dev));
+        (void)hipFree(stacked);
+        (void)hipFree(frames);
+        (void)hipFree(d_lists);
+    }
+    return 0;
+}

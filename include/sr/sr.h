@@ -316,6 +316,43 @@ int sr_render_block_list(sr_ctx* ctx, const sr_camera* cams, int n_frames, const
 int sr_wave_costs(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width, int height,
                   int32_t* dev_out, sr_stream stream);
 
+/* ---- Multi-GPU frame partition (not in the reference, whose frame is one
+ * draw on one GPU, src/main.cpp:318-319). A frame's rows are cut
+ * into blocks of block_rows (8: one 8x8 wave tile tall); every rank of a node
+ * renders an equal-length list of blocks of about equal cost with
+ * sr_render_block_list, the tiles are gathered to the root (the caller's
+ * RCCL collective: ncclGather of equal-size tiles, examples/sr_multi_gpu.cpp)
+ * and sr_assemble_blocks puts the frame back together. */
+
+/* Per-block cost from an sr_wave_costs map copied to the host
+ * ([n_blocks][waves_per_block][2] = {steps, events} per 8x8 wave): out_cost[b]
+ * = sum over the block's waves of steps + event_steps x events (a wave runs
+ * until its longest ray ends; a budget event costs about 8 wave-steps,
+ * DESIGN.md §8). Same values as dist.block_costs. */
+int sr_block_costs(const int32_t* wave_cost, int n_blocks, int waves_per_block, double event_steps,
+                   double* out_cost);
+
+/* Equal-length block lists of about equal cost for `world` ranks:
+ * out_lists[r * per + s] (-1: padding), *out_per = ceil(n_blocks / world);
+ * SR_E_CAPACITY when world * per > max_entries. Blocks by descending cost to
+ * the least-loaded rank with room, then pairwise swaps out of the most
+ * loaded rank while one lowers the pair's maximum; the block-cyclic lists
+ * when they are at least as even. Deterministic, binary64, the same lists as
+ * dist.balanced_blocks: every rank derives identical lists from identical
+ * costs (or the root computes and broadcasts them). */
+int sr_balanced_blocks(const double* cost, int n_blocks, int world, int* out_lists, int max_entries, int* out_per);
+
+/* Reassembles n_frames frames from gathered tiles: rank r's tile of frame f
+ * starts at stacked + r * rank_stride + f * in_frame_stride, its slot s holds
+ * the block_rows rows of frame block lists[r * per + s] (dense rows of
+ * row_bytes); frame f's row y lands at out + f * out_frame_stride + y *
+ * row_bytes (rows >= height dropped, -1 slots skipped). on_device != 0: every
+ * pointer, `lists` included, is device memory and the copy is a kernel on
+ * `stream` (asynchronous); 0: host memory, synchronous. */
+int sr_assemble_blocks(const uint8_t* stacked, size_t rank_stride, size_t in_frame_stride, const int* lists,
+                       int world, int per, int height, int block_rows, size_t row_bytes, uint8_t* out,
+                       size_t out_frame_stride, int n_frames, int on_device, sr_stream stream);
+
 /* Debug/parity variant: unclamped FragColor as float RGBA (dev_rgba32, may be
  * NULL), the RGBA8 pixel (dev_rgba8, may be NULL) and the number of executed
  * geodesic steps per pixel (dev_steps, may be NULL). Dense rows. */

@@ -686,7 +686,30 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
 
 }  // namespace
 
+extern "C" hipError_t sr_assemble_blocks_device(const uint8_t* stacked, size_t rank_stride, size_t in_frame_stride,
+                                                const int* dev_lists, int world, int per, int height, int block_rows,
+                                                size_t row_bytes, uint8_t* out, size_t out_frame_stride, int n_frames,
+                                                hipStream_t stream);
+extern "C" int sr_assemble_blocks_host(const uint8_t* stacked, size_t rank_stride, size_t in_frame_stride,
+                                       const int* lists, int world, int per, int height, int block_rows,
+                                       size_t row_bytes, uint8_t* out, size_t out_frame_stride, int n_frames);
+
 extern "C" {
+
+int sr_assemble_blocks(const uint8_t* stacked, size_t rank_stride, size_t in_frame_stride, const int* lists,
+                       int world, int per, int height, int block_rows, size_t row_bytes, uint8_t* out,
+                       size_t out_frame_stride, int n_frames, int on_device, sr_stream stream) {
+    if (!stacked || !lists || !out || world <= 0 || per < 0 || height <= 0 || block_rows <= 0 || row_bytes == 0 ||
+        n_frames < 1)
+        return SR_E_INVALID;
+    if (!on_device)
+        return sr_assemble_blocks_host(stacked, rank_stride, in_frame_stride, lists, world, per, height, block_rows,
+                                       row_bytes, out, out_frame_stride, n_frames);
+    const hipError_t e = sr_assemble_blocks_device(stacked, rank_stride, in_frame_stride, lists, world, per, height,
+                                                   block_rows, row_bytes, out, out_frame_stride, n_frames,
+                                                   reinterpret_cast<hipStream_t>(stream));
+    return hip_ok(e) ? SR_OK : SR_E_HIP;
+}
 
 const char* sr_version(void) { return "schwarzschild-mi355x 0.1 (gfx950)"; }
 

@@ -25,7 +25,11 @@ peer's tile travels over its own xGMI link into rank 0.
 """
 from __future__ import annotations
 
+import ctypes as C
+
 import numpy as np
+
+from . import abi
 
 
 def nblocks(height: int, block_rows: int) -> int:
@@ -63,15 +67,41 @@ def wave_costs(steps, block_rows: int = 8, wave: int = 8):
 EVENT_STEPS = 8.0  # one budget event costs about as much as this many wave steps (profiles/r02/s15_*)
 
 
-def block_costs(wave_cost, event_steps: float = EVENT_STEPS):
+def block_costs_py(wave_cost, event_steps: float = EVENT_STEPS):
     """Per 8-row block cost from sr_wave_costs' [rows / 8, cols / 8, 2] map:
-    the sum over the block's waves of steps + event_steps x events."""
+    the sum over the block's waves of steps + event_steps x events (the
+    statement of the rule; block_costs runs the library's sr_block_costs)."""
     w = wave_cost.cpu().numpy() if hasattr(wave_cost, "cpu") else np.asarray(wave_cost)
     w = w.astype(np.float64)
     return (w[..., 0] + event_steps * w[..., 1]).sum(axis=1)
 
 
+def block_costs(wave_cost, event_steps: float = EVENT_STEPS):
+    """block_costs_py through the C-ABI (sr_block_costs, csrc/host/partition.cpp):
+    the C++ a multi-GPU caller of libsr uses."""
+    w = wave_cost.cpu().numpy() if hasattr(wave_cost, "cpu") else np.asarray(wave_cost)
+    w = np.ascontiguousarray(w, dtype=np.int32)
+    nb, nc = w.shape[0], w.shape[1]
+    out = np.zeros(nb, dtype=np.float64)
+    abi.check(abi.load().sr_block_costs(w.ctypes.data, nb, nc, float(event_steps), out.ctypes.data), "sr_block_costs")
+    return out
+
+
 def balanced_blocks(costs, world: int) -> list[list[int]]:
+    """balanced_blocks_py through the C-ABI (sr_balanced_blocks,
+    csrc/host/partition.cpp): the same lists, computed by the library."""
+    c = np.ascontiguousarray(np.asarray(costs, dtype=np.float64))
+    nb = int(c.shape[0])
+    per = (nb + world - 1) // world
+    out = np.empty(max(1, world * per), dtype=np.int32)
+    got = C.c_int()
+    abi.check(abi.load().sr_balanced_blocks(c.ctypes.data, nb, int(world), out.ctypes.data, int(out.size),
+                                            C.byref(got)), "sr_balanced_blocks")
+    assert got.value == per
+    return [[int(b) for b in out[r * per:(r + 1) * per]] for r in range(world)]
+
+
+def balanced_blocks_py(costs, world: int) -> list[list[int]]:
     """Equal-length block lists (padded with -1) of about equal total cost:
     blocks by descending cost, each to the rank with the least cost so far
     among those with room (ties: lowest rank), then pairwise swaps (a pad
@@ -169,6 +199,45 @@ def assemble_lists(stacked, lists, height: int, block_rows: int, src=None):
     return v.reshape((nb * block_rows,) + rest)[:height]
 
 
+def assemble_blocks_abi(stacked, lists, height: int, block_rows: int, out=None, dev_lists=None, stream=None):
+    """assemble_lists through the C-ABI (sr_assemble_blocks): gathered tiles
+    [world, B, tile_rows, W, C] (or [world, tile_rows, W, C]) -> frames
+    [B, height, W, C] (or [height, W, C]). Torch tensors on a device: the
+    library's copy kernel on `stream` (dev_lists: the flattened lists as an
+    int32 tensor on that device); numpy arrays: the host copy."""
+    world, per = len(lists), len(lists[0])
+    batched = stacked.ndim == 5
+    B = stacked.shape[1] if batched else 1
+    tile_rows, W, ch = stacked.shape[-3], stacked.shape[-2], stacked.shape[-1]
+    is_torch = type(stacked).__module__.startswith("torch")
+    row_bytes = W * ch * (stacked.element_size() if is_torch else stacked.itemsize)
+    in_frame = tile_rows * row_bytes
+    rank_stride = B * in_frame
+    lib = abi.load()
+    if is_torch and stacked.device.type == "cuda":
+        import torch
+
+        assert stacked.is_contiguous()
+        if out is None:
+            out = torch.empty((B, height, W, ch), dtype=stacked.dtype, device=stacked.device)
+        if dev_lists is None:
+            dev_lists = torch.tensor([b for l in lists for b in l], dtype=torch.int32, device=stacked.device)
+        s = stream if stream is not None else torch.cuda.current_stream(stacked.device)
+        abi.check(lib.sr_assemble_blocks(C.c_void_p(stacked.data_ptr()), rank_stride, in_frame,
+                                         C.c_void_p(dev_lists.data_ptr()), world, per, height, block_rows, row_bytes,
+                                         C.c_void_p(out.data_ptr()), height * row_bytes, B, 1,
+                                         C.c_void_p(s.cuda_stream)), "sr_assemble_blocks")
+        return out if batched else out[0]
+    a = stacked.numpy() if hasattr(stacked, "numpy") else np.asarray(stacked)
+    a = np.ascontiguousarray(a)
+    res = np.zeros((B, height, W, ch), dtype=a.dtype) if out is None else out
+    flat = np.ascontiguousarray([b for l in lists for b in l], dtype=np.int32)
+    abi.check(lib.sr_assemble_blocks(a.ctypes.data, rank_stride, in_frame, flat.ctypes.data, world, per, height,
+                                     block_rows, row_bytes, res.ctypes.data, height * row_bytes, B, 0, None),
+              "sr_assemble_blocks")
+    return res if batched else res[0]
+
+
 def assemble(stacked, world: int, height: int, block_rows: int):
     """[world, tile_rows, W, C] gathered tiles (rank order) -> [height, W, C]
     frame. numpy arrays or torch tensors. Batched tiles [world, B, tile_rows,
@@ -201,7 +270,9 @@ class FrameGather:
     def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None, lists=None):
         self.world, self.rank, self.height, self.block_rows, self.group = world, rank, height, block_rows, group
         self.lists = lists  # balanced_blocks lists (sr_render_block_list tiles), else block-cyclic
-        self._src = None  # the lists' block sources on the tiles' device (made once)
+        self._src = None  # the lists' block sources on the tiles' device (made once; host tiles)
+        self._dev_lists = None  # the flattened lists on the tiles' device (sr_assemble_blocks)
+        self._frames = None  # rank 0's reassembled frames (device tiles)
         self.tile = tile
         self.stacked = None
         self.views = None
@@ -214,10 +285,14 @@ class FrameGather:
         device now, outside any launch."""
         self.lists = lists
         self._src = None
-        if hasattr(self.tile, "device"):
+        self._dev_lists = None
+        if type(self.tile).__module__.startswith("torch"):
             import torch
 
             self._src = torch.as_tensor(list_sources(lists, self.height, self.block_rows), device=self.tile.device)
+            if self.tile.device.type == "cuda":
+                self._dev_lists = torch.tensor([b for l in lists for b in l], dtype=torch.int32,
+                                               device=self.tile.device)
 
     def __call__(self, n: int | None = None, assemble_frame: bool = True):
         import torch.distributed as dist
@@ -236,11 +311,26 @@ class FrameGather:
         if not assemble_frame:
             return stacked
         if self.lists is not None:
+            if type(stacked).__module__.startswith("torch") and stacked.device.type == "cuda":
+                # the library's reassembly kernel on the launch's stream, into
+                # this gather's frame buffer (valid until its next call)
+                if self._dev_lists is None or self._dev_lists.device != stacked.device:
+                    import torch
+
+                    # built once: a per-call host-to-device copy of the lists
+                    # would wait for the launch's stream (the whole render)
+                    self._dev_lists = torch.tensor([b for l in self.lists for b in l], dtype=torch.int32,
+                                                   device=stacked.device)
+                nf = stacked.shape[1] if stacked.ndim == 5 else 1
+                if self._frames is None or self._frames.shape[0] < nf:
+                    self._frames = stacked.new_empty((nf, self.height) + tuple(stacked.shape[-2:]))
+                out = assemble_blocks_abi(stacked if stacked.is_contiguous() else stacked.contiguous(), self.lists,
+                                          self.height, self.block_rows, out=self._frames[:nf],
+                                          dev_lists=self._dev_lists)
+                return out
             if self._src is None or self._src.device != stacked.device:
                 import torch
 
-                # built once: a per-call host-to-device copy of the index would
-                # wait for the launch's stream (the frame's whole render)
                 self._src = torch.as_tensor(list_sources(self.lists, self.height, self.block_rows),
                                             device=stacked.device)
             return assemble_lists(stacked, self.lists, self.height, self.block_rows, self._src)

@@ -7,7 +7,8 @@ build container and committed, per row, sha256 of the RGBA8 bytes and of the
 int32 executed-step counts (tests/golden/frame_hashes.npz). Here the GPU
 renders the same frames - through the paths bench.py uses: batched launches
 with a learned launch order, and config 4 as its eight cost-balanced rank
-shares reassembled by dist.assemble_lists - and every row hash must be equal.
+shares reassembled by the library's sr_assemble_blocks - and every row hash
+must be equal.
 No tolerance: the arithmetic contract makes the kernel's
 pixels the oracle's bit for bit. Mismatching rows are re-run through the
 oracle for the failure message.
@@ -134,7 +135,8 @@ def test_config4_rank_shares_assembled(pkg, fh, assets):
     """Config 4 (3840x2160, 4000 steps, row-tiled over 8 GPUs): the eight
     cost-balanced rank shares of bench.py (sr_wave_costs -> dist.block_costs
     -> balanced_blocks -> sr_render_block_list, two frames per launch)
-    reassembled by dist.assemble_lists, and the step map of the debug render."""
+    reassembled by sr_assemble_blocks on the device, and the step map of the
+    debug render."""
     import torch
 
     W, H, N = (int(v) for v in fh["c4/config"])
@@ -152,8 +154,14 @@ def test_config4_rank_shares_assembled(pkg, fh, assets):
     for lst in lists:
         for _ in range(2):  # the second launch runs the list's learned order
             t = r.render_block_list([cam, cam], params, W, H, BLOCK_ROWS, lst)
-        tiles.append(t.cpu().numpy())
-    frames = D.assemble_lists(np.stack(tiles), lists, H, BLOCK_ROWS)
+        tiles.append(t.clone())
+    # the root's reassembly: the library's kernel (sr_assemble_blocks, as bench.py's
+    # FrameGather runs it) and dist.assemble_lists' statement of it
+    stacked = torch.stack(tiles)
+    frames = D.assemble_blocks_abi(stacked, lists, H, BLOCK_ROWS)
+    torch.cuda.synchronize()
+    frames = frames.cpu().numpy()
+    assert np.array_equal(frames, D.assemble_lists(stacked.cpu().numpy(), lists, H, BLOCK_ROWS))
     for f in range(2):
         compare(pkg, fh, "c4", frames[f], None, f"8 rank shares, frame {f}")
     r.close()
@@ -179,3 +187,34 @@ def test_config5_still_8k(pkg, fh, assets):
     torch.cuda.synchronize()
     compare(pkg, fh, "c5", out.cpu().numpy(), None, "second frame")
     r.close()
+
+
+def test_cpp_multi_gpu_driver_frame(pkg, fh, assets, tmp_path):
+    """examples/sr_multi_gpu (C++ over the C-ABI, RCCL): the node-level path -
+    sr_wave_costs -> sr_block_costs -> sr_balanced_blocks, sr_render_block_list
+    per GPU, ncclGather of the tiles (ncclCommInitAll over the box's one GPU),
+    sr_assemble_blocks - renders the headline frame with the reference's
+    textures (raw files) equal row for row to the oracle fixture."""
+    import json
+    import subprocess
+
+    exe = Path(__file__).resolve().parents[1] / "examples" / "bin" / "sr_multi_gpu"
+    if not exe.exists():
+        pytest.skip("examples/bin/sr_multi_gpu not built")
+    W, H, N = (int(v) for v in fh["c3/config"])
+    sky, arr = assets["2k"], assets["arr"]
+    (tmp_path / "sky.rgb").write_bytes(np.ascontiguousarray(sky).tobytes())
+    a = np.ascontiguousarray(arr)
+    if a.shape[-1] == 3:
+        a = np.concatenate([a, np.full(a.shape[:-1] + (1,), 255, np.uint8)], axis=-1)
+    (tmp_path / "arr.rgba").write_bytes(a.tobytes())
+    out = tmp_path / "frame.rgba"
+    cmd = [str(exe), "--gpus", "1", "--width", str(W), "--height", str(H), "--max-steps", str(N), "--frames", "4",
+           "--batch", "2", "--warmup", "2", "--skybox", f"{tmp_path / 'sky.rgb'}:{sky.shape[1]}:{sky.shape[0]}",
+           "--array", f"{tmp_path / 'arr.rgba'}:{a.shape[2]}:{a.shape[1]}:{a.shape[0]}", "--out-raw", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["world_size"] == 1 and line["frames"] == 4 and line["ranks"][0]["render_ms_per_frame"] > 0
+    frame = np.frombuffer(out.read_bytes(), dtype=np.uint8).reshape(H, W, 4)
+    compare(pkg, fh, "c3", frame, None, "C++ RCCL driver")
