@@ -93,11 +93,14 @@ typedef struct {
     float a2[3], cn;  // cn: |bc| x 1.001, rounded up (outward_clear)
 } sr_dev_slot;  // 128 B
 
-// Per-pixel state planes passed between the integrate / shade / resume kernels
-// (geodesic.hip PS_*): status, step, steps, hit count, frag[4], ro, rd, nv, tv,
-// u, du, then SR_PS_HITS hit records {p[3], slot * 8 + face, chord dir[3], steps}.
+// Per-pixel state passed between the integrate / shade / resume kernels
+// (geodesic.hip PS_*), floats per pixel: a 16-byte record {packed word
+// (status, hit count, steps), rd[3]}, SR_PS_HITS 32-byte hit
+// records {p[3], key | steps << 8, chord dir[3], -}, then planes of the
+// resumable / flat-ray state (step, frag[4], ro, nv, tv, u, du). Written only
+// where the next kernel reads them.
 #define SR_PS_HITS 4
-#define SR_PS_FIELDS (24 + 8 * SR_PS_HITS)
+#define SR_PS_FIELDS (4 + 8 * SR_PS_HITS + 16)
 // Texture-array opacity bitmap radius (texels), see sr_api.cpp make_opacity_map
 #define SR_OPQ_RADIUS 2
 
@@ -181,6 +184,11 @@ typedef struct {
     int32_t split_tiles;
     int32_t split_log2;
     int32_t split_min_steps;
+    // two rays per lane (sr_integrate_pair_kernel): on, and the LDS rows per
+    // ray of the packed budget layout (1 + budget slots + 3 x budgeted
+    // cylinders, at least SR_MAX_BUDGET + 1)
+    int32_t pair;
+    int32_t pair_rows;
 } sr_dev_frame;
 
 #endif

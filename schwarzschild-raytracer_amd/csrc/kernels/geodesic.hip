@@ -552,8 +552,10 @@ struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
-    float mh;     // min_k of the cylinders' slab budgets H[k] (E[SR_E_SLAB0 + k]): the bound that
+    float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
                   // covers chords nearly parallel to an axis
+    int pa0, slab0;  // LDS rows of pa[0] and H[0]: SR_E_PA0 / SR_E_SLAB0 (static layout), or packed
+                     // after the scene's budget slots (sr_integrate_pair_kernel)
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -577,8 +579,8 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         if (c) {
             const f3 ax = ld3(sc->slots[__builtin_ctz(c)].a1);
             const float pa = dot(nv, ax), pb = dot(tv, ax);
-            bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE] = pa;
-            bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
+            bs.E[(bs.pa0 + 2 * k) * SR_E_STRIDE] = pa;
+            bs.E[(bs.pa0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
             // NaN frames keep the test (the comparison is false)
             cm |= (uint32_t)(!(pa * pa + pb * pb < 1.0f - 2.0f * SR_BUDGET_DPMIN - 1.0e-3f)) << k;
             c &= c - 1;
@@ -622,7 +624,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
             const float e = clearance_slab(sc->slots[__builtin_ctz(c)], A, a);
-            bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = e;
+            bs.E[(bs.slab0 + k) * SR_E_STRIDE] = e;
             mh = nmin(mh, e);
             c &= c - 1;
         }
@@ -642,8 +644,8 @@ __device__ __forceinline__ CylDirs cyl_dirs(const sr_dev_scene* __restrict__ sc,
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         d.pa[k] = d.pb[k] = 0.0f;
         if (c) {
-            d.pa[k] = bs.E[(SR_E_PA0 + 2 * k) * SR_E_STRIDE];
-            d.pb[k] = bs.E[(SR_E_PA0 + 1 + 2 * k) * SR_E_STRIDE];
+            d.pa[k] = bs.E[(bs.pa0 + 2 * k) * SR_E_STRIDE];
+            d.pb[k] = bs.E[(bs.pa0 + 1 + 2 * k) * SR_E_STRIDE];
             c &= c - 1;
         }
     }
@@ -771,8 +773,17 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     float e[NS], h[SR_MAX_CYLINDERS];
 #pragma unroll
     for (int j = 0; j < NS; j++) e[j] = bs.E[j * SR_E_STRIDE];
+    {
+        uint32_t c = cyl;  // only the scene's cylinders' rows exist in the packed layout
 #pragma unroll
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) h[k] = bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE];
+        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+            h[k] = INFINITY;
+            if (c) {
+                h[k] = bs.E[(bs.slab0 + k) * SR_E_STRIDE];
+                c &= c - 1;
+            }
+        }
+    }
     uint32_t forced = 0;  // this lane's slots whose E does not cover the chord
     {
         uint32_t c = cyl;
@@ -829,7 +840,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (c) {
                 if (!((spent >> (__builtin_ctz(c) + 1)) & 1u)) {
                     const float v = h[k] - T;
-                    bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = v;
+                    bs.E[(bs.slab0 + k) * SR_E_STRIDE] = v;
                     mh = nmin(mh, v);
                 }
                 c &= c - 1;
@@ -887,7 +898,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (TY == SR_OBJECT_CYLINDER) {
                 const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
                 const float vh = clearance_slab(st, B, a) - perr;
-                bs.E[(SR_E_SLAB0 + k) * SR_E_STRIDE] = vh;
+                bs.E[(bs.slab0 + k) * SR_E_STRIDE] = vh;
                 mh = nmin(mh, vh);
             }
             if (__ballot(h) && __ballot(h && slot_reachable(&st, j, A, B, perr))) reach |= 1u << j;
@@ -1385,12 +1396,33 @@ __device__ __forceinline__ uint32_t unorm8(float x) {
 #define ST_MORE 2  // stopped with SR_PS_HITS translucent hits recorded
 #define ST_FLAT 3  // unbounded intersect(ray), then get_bg if alpha != 1 (frag:874-876, 895-897, 903-905)
 #define ST_BG 4    // get_bg(rd) (frag:921-922 break, 935)
+#define ST_BH 5    // stopped in the black hole (opaque black) after the logged hits
 
+// The hand-off is written only where the next kernel reads it, in records
+// that one lane writes whole (partial writes of shared sectors by scattered
+// lanes cost whole sectors: as SoA planes the sparse hit records made the
+// hand-off 2.4x its size):
+//   every pixel      one 16-byte store {packed word, rd} (rd: the final
+//                    direction, read by escaped and flat rays)
+//   logged hits      one 32-byte record each {p, key | steps << 8, dir}; a
+//                    ray that ends in the black hole gets status ST_BH
+//                    instead (its colour is a constant, shade_hit)
+//   ST_FLAT          ro (plane)
+//   ST_MORE          the resumable state (planes): the log filled with
+//                    translucent hits; sr_resume_kernel continues the ray
+// An ST_HIT pixel's last logged hit is opaque exactly (hit_opacity), so the
+// shade kernel always finishes it: it keeps no resumable state.
 enum {
-    PS_STATUS = 0, PS_I = 1, PS_STEPS = 2, PS_NHITS = 3, PS_FRAG = 4, PS_RO = 8, PS_RD = 11, PS_NV = 14, PS_TV = 17,
-    PS_U = 20, PS_DU = 21, PS_HIT0 = 24, PS_HIT_STRIDE = 8  // hit j: p[3], slot * 8 + face, chord dir[3], steps
+    PS_REC = 0,                       // [4 floats / px] word, rd[3]
+    PS_HITS = 4,                      // [8 floats / hit] p[3], (key + 24) | steps << 8, dir[3], -
+    PS_PLANES = 4 + 8 * SR_PS_HITS,   // planes (field * n + id) from here:
+    PS_I = 0, PS_FRAG = 1, PS_RO = 5, PS_NV = 8, PS_TV = 11, PS_U = 14, PS_DU = 15
 };
-static_assert(PS_HIT0 + PS_HIT_STRIDE * SR_PS_HITS == SR_PS_FIELDS, "pixel-state layout");
+static_assert(PS_PLANES + 16 == SR_PS_FIELDS, "pixel-state layout");
+// key = slot * 8 + face in [-24, 167]: slots -3 .. SR_MAX_OBJECTS - 1
+#define PS_KEY_BIAS 24
+static_assert((SR_MAX_OBJECTS - 1) * 8 + 7 + PS_KEY_BIAS < 256, "hit key fits 8 bits");
+__device__ __forceinline__ int ps_word(int st, int nh, int steps) { return st | (nh << 3) | (steps << 8); }
 
 struct Ray {
     f3 ro, rd, nv, tv;
@@ -1430,7 +1462,16 @@ __device__ __forceinline__ bool pixel_of(const sr_dev_frame& fr, int block, int 
 struct PS {
     float* __restrict__ p;
     size_t n;
-    __device__ __forceinline__ float& at(int f, size_t id) const { return p[(size_t)f * n + id]; }
+    // the 16-byte record and the hit records (one lane, whole records)
+    __device__ __forceinline__ void put_rec(size_t id, int w, f3 rd) const {
+        *reinterpret_cast<float4*>(p + 4 * id) = make_float4(__int_as_float(w), rd.x, rd.y, rd.z);
+    }
+    __device__ __forceinline__ float4 get_rec(size_t id) const { return *reinterpret_cast<const float4*>(p + 4 * id); }
+    __device__ __forceinline__ float* hit(size_t id, int j) const {
+        return p + 4 * n + (id * SR_PS_HITS + (size_t)j) * 8;
+    }
+    // planes of the resumable / flat-ray state
+    __device__ __forceinline__ float& at(int f, size_t id) const { return p[(size_t)(PS_PLANES + f) * n + id]; }
     __device__ __forceinline__ void put3(int f, size_t id, f3 v) const {
         at(f, id) = v.x;
         at(f + 1, id) = v.y;
@@ -1592,6 +1633,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     __shared__ float lds_E[SR_E_ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     Budget bs;
     bs.E = lds_E + threadIdx.x;
+    bs.pa0 = SR_E_PA0;
+    bs.slab0 = SR_E_SLAB0;
     if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
@@ -1880,11 +1923,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_PT(5);
                 if (op == OP_ZERO) break;  // frag + vec4(0), alpha != 1: the ray goes on (frag:930-932)
                 if (!RECORD) return ST_HIT;
-                const int f = PS_HIT0 + PS_HIT_STRIDE * log.n;
-                log.ps.put3(f, log.id, hit.p);
-                log.ps.puti(f + 3, log.id, hit.slot * 8 + hit.face);
-                log.ps.put3(f + 4, log.id, r.rd);
-                log.ps.puti(f + 7, log.id, r.steps);  // the ray's step count if this hit ends it
+                if (hit.slot == SLOT_BH) return ST_BH;  // opaque black (shade_hit): no record
+                // r.steps: the ray's step count if this hit ends it
+                float* h = log.ps.hit(log.id, log.n);
+                h[0] = hit.p.x;
+                h[1] = hit.p.y;
+                h[2] = hit.p.z;
+                h[3] = __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (r.steps << 8));
+                h[4] = r.rd.x;
+                h[5] = r.rd.y;
+                h[6] = r.rd.z;
                 log.n++;
                 if (op == OP_OPAQUE) return ST_HIT;
                 if (log.n == SR_PS_HITS) return ST_MORE;
@@ -1896,6 +1944,371 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     r.steps = sbase + N;
     settle_prev(N);
     return ST_BG;
+}
+
+// ---- two rays per lane (sr_integrate_pair_kernel) ------------------------------
+// The fast loop is bound by one wave's dependency chain: RK4 (~21 dependent
+// VALU), the radius reciprocal, the chord bound's square root, the compare and
+// the exit branch, which six waves per SIMD do not hide. Here
+// each lane carries two rays - the pixels of two vertically adjacent 8x8 wave
+// tiles - that share the wave-uniform step index and step-table loads: their
+// RK4s run as packed pairs ACROSS the rays ((uA, uB), (u'A, u'B): the same
+// IEEE operations per ray as rk4_step, so bit-identical), two independent
+// chains per lane in ~1.4x the instructions of one.
+// Each ray keeps its own state and clearance budgets (its own LDS columns);
+// the slow path is one copy of the single-ray code run for ray A, then - with
+// the two rays' registers swapped - for ray B, only for a ray set in which
+// some lane needs attention. A ray that ends writes its pixel record and
+// parks on the circular photon orbit (u = 2/3 exactly, u' = 0: ddu = -0, so
+// RK4 leaves it fixed) with an infinite limit, so it never triggers an exit.
+// Every per-ray decision is the single-ray kernel's (each ray's budget events
+// are those of its own 64-ray set), so pixels are bit-identical to it.
+// LDS rows per ray: E[0..nb], pa/pb and H of the budgeted cylinders; at least
+// the 9 rows budget_event reads unconditionally
+#define SR_PAIR_ROWS(nb, ncyl) (1 + (nb) + 3 * (ncyl) > SR_MAX_BUDGET + 1 ? 1 + (nb) + 3 * (ncyl) : SR_MAX_BUDGET + 1)
+struct PairRay {
+    Ray r;                  // ro, rd, nv, tv, u, du (the step index is the wave's)
+    float T, m, mh;         // Budget scalars
+    uint32_t cm;
+    float up, rA;           // chord bookkeeping (integrate)
+    int im;
+    int st;                 // -1 while alive, else its status (the pixel record is written)
+    int n;                  // logged hits
+    bool force;
+    float un, dun, rB, Tn, lim;  // step i as the fast loop left it
+    uint32_t par;
+};
+
+__device__ __forceinline__ void swap_rays(PairRay& a, PairRay& b) {
+    PairRay t = a;
+    a = b;
+    b = t;
+}
+
+__device__ __forceinline__ void rk4_pair(v2f u, v2f du, float h, float hh, float h6, v2f& un, v2f& dun) {
+    const v2f H1 = {h, h}, H2 = {hh, hh}, HS = {h6, h6}, two = {2.0f, 2.0f}, k15 = {1.5f, 1.5f}, one = {1.0f, 1.0f};
+    auto ddu2 = [&](v2f x) { return -x * (one - k15 * x); };
+    const v2f k1 = du, l1 = ddu2(u);
+    const v2f k2 = du + l1 * H2, l2 = ddu2(u + k1 * H2);
+    const v2f k3 = du + l2 * H2, l3 = ddu2(u + k2 * H2);
+    const v2f k4 = du + l3 * H1, l4 = ddu2(u + k3 * H1);
+    un = u + HS * (__builtin_elementwise_fma(two, k3, __builtin_elementwise_fma(two, k2, k1)) + k4);
+    dun = du + HS * (__builtin_elementwise_fma(two, l3, __builtin_elementwise_fma(two, l2, l1)) + l4);
+}
+
+// The pixel record of a ray that has ended (sr_integrate_kernel's hand-off).
+__device__ __forceinline__ void pair_finish(const PS& ps, size_t id, PairRay& L, int st, int steps, int i) {
+    ps.put_rec(id, ps_word(st, L.n, steps), L.r.rd);
+    if (st == ST_FLAT || st == ST_MORE) ps.put3(PS_RO, id, L.r.ro);
+    if (st == ST_MORE) {
+        ps.puti(PS_I, id, i);
+        ps.put3(PS_NV, id, L.r.nv);
+        ps.put3(PS_TV, id, L.r.tv);
+        ps.at(PS_U, id) = L.r.u;
+        ps.at(PS_DU, id) = L.r.du;
+    }
+    L.st = st;
+    L.r.u = 2.0f / 3.0f;  // the circular photon orbit: ddu(u) = -0, RK4 keeps it
+    L.r.du = 0.0f;
+    L.m = INFINITY;
+    L.mh = INFINITY;
+    L.cm = 0u;
+    L.force = false;
+}
+
+// Budget views of a PairRay (the single-ray helpers take a Budget); E: the
+// ray's LDS columns, rows packed after the scene's budget slots
+__device__ __forceinline__ Budget pair_budget(const PairRay& L, float* E, int pa0, int slab0) {
+    Budget bs;
+    bs.E = E;
+    bs.pa0 = pa0;
+    bs.slab0 = slab0;
+    bs.T = L.T;
+    bs.m = L.m;
+    bs.mh = L.mh;
+    bs.cm = L.cm;
+    return bs;
+}
+__device__ __forceinline__ void pair_store_budget(PairRay& L, const Budget& bs) {
+    L.T = bs.T;
+    L.m = bs.m;
+    L.mh = bs.mh;
+    L.cm = bs.cm;
+}
+
+// Both rays of every lane from step 0 (sr_integrate_pair_kernel): A = ray
+// slot 0, B = slot 1; alive rays have passed init_pixel. Writes the pixel
+// records; returns the lane's largest step count.
+__device__ __forceinline__ int integrate_pair(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                              const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
+                                              const PS& ps, size_t idA, size_t idB, float* E0, PairRay& A,
+                                              PairRay& B) {
+    const int N = fr.max_steps;
+    const int nb = sc->num_budget, ncyl = __builtin_popcount((unsigned)sc->budget_cyl_mask);
+    const int rows = SR_PAIR_ROWS(nb, ncyl);
+    const int pa0 = nb + 1, slab0 = nb + 1 + 2 * ncyl;
+    float* const EB = E0 + (size_t)rows * SR_E_STRIDE;  // ray B's columns
+    int smax = 0;
+    auto phi_cs = [&](int j) -> f2 {
+        if (j < 0) return F2(1.0f, 0.0f);
+        const float4 t = tbl[2 * j];
+        return F2(t.z, t.w);
+    };
+    // materialise ray L's chord of step i - 1
+    auto settle_prev = [&](PairRay& L, int i) {
+        if (L.im == i - 1) return;
+        const f2 p1 = phi_cs(i - 1);
+        f3 Aq;
+        if (L.im == i - 2) {
+            Aq = L.r.ro;
+        } else {
+            const f2 p2 = phi_cs(i - 2);
+            Aq = point_at(L.r, L.up, p2.x, p2.y);
+        }
+        f3 Bq = point_at(L.r, L.r.u, p1.x, p1.y);
+        f3 delta = Bq - Aq;
+        float seg = len(delta);
+        L.r.rd = delta / seg;
+        L.r.ro = Bq;
+        L.im = i - 1;
+    };
+    auto finish = [&](PairRay& L, int k, int st, int steps, int i) {
+        pair_finish(ps, k ? idB : idA, L, st, steps, i);
+        smax = max(smax, steps);
+    };
+    // One copy of a per-ray body for ray A, then for ray B with the two rays'
+    // registers swapped (f(L, k): L is the current ray, k its slot); a set in
+    // which no lane's `need` holds is skipped.
+#ifdef SR_PAIR_SWAP
+    auto each = [&](auto need, auto f) {
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < 2; k++) {
+            if (k == 1) {
+                if (!__ballot(need(B))) break;
+                swap_rays(A, B);
+            } else if (!__ballot(need(A))) {
+                continue;
+            }
+            f(A, k);
+            if (k == 1) swap_rays(A, B);
+        }
+    };
+#else
+    auto each = [&](auto need, auto f) {
+        if (__ballot(need(A))) f(A, 0);
+        if (__ballot(need(B))) f(B, 1);
+    };
+#endif
+    int i = 0;
+    for (;;) {
+        i = __builtin_amdgcn_readfirstlane(i);
+        if (i >= N) break;
+        // frag:891-912 at the top of step i, per ray
+        each([&](const PairRay& L) { return L.st < 0 && L.r.u < fr.u_f; },
+             [&](PairRay& L, int k) {
+                 if (L.st < 0 && L.r.u < fr.u_f) {
+                     settle_prev(L, i);
+                     f3 q;
+                     if (!sphere_test(L.r.ro, L.r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) {
+                         finish(L, k, ST_FLAT, i + 1, i);
+                         return;
+                     }
+                     L.r.nv = nrm(q);
+                     if (fabsf(dot(L.r.rd, L.r.nv)) >= 1.0f - SR_EPS) {
+                         finish(L, k, ST_FLAT, i + 1, i);
+                         return;
+                     }
+                     L.r.tv = nrm(cross(cross(L.r.nv, L.r.rd), L.r.nv));
+                     L.r.u = 1.0f / len(q);
+                     L.r.du = -L.r.u * dot(L.r.rd, L.r.nv) / dot(L.r.rd, L.r.tv);
+                     Budget bs = pair_budget(L, k ? EB : E0, pa0, slab0);
+                     budget_frame(sc, bs, L.r.nv, L.r.tv);
+                     pair_store_budget(L, bs);
+                     L.force = true;
+                 }
+             });
+        if (A.st >= 0 && B.st >= 0) break;  // both rays of this lane have ended
+        // ---- fast loop over both rays (see integrate)
+        const float lA0 = A.st >= 0 ? INFINITY : (A.force ? -INFINITY : A.m);
+        const float lB0 = B.st >= 0 ? INFINITY : (B.force ? -INFINITY : B.m);
+        const bool any_cm = __ballot((A.cm | B.cm) != 0u);
+        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
+        float4 e;
+        auto fast = [&](auto cm_tag) {
+            constexpr bool CM = decltype(cm_tag)::value;
+            A.lim = lA0;
+            B.lim = lB0;
+            A.par = B.par = 0;
+            e = ldc(tp);
+            float4 e1 = ldc(tp + 1);
+            f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);
+            Budget ba = pair_budget(A, E0, pa0, slab0), bb = pair_budget(B, EB, pa0, slab0);
+            const CylDirs cda = CM ? cyl_dirs(sc, ba) : CylDirs{};
+            const CylDirs cdb = CM ? cyl_dirs(sc, bb) : CylDirs{};
+            if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            auto compute = [&]() -> bool {
+                v2f un, dun;
+                rk4_pair(v2f{A.r.u, B.r.u}, v2f{A.r.du, B.r.du}, e.x, e1.y, e.y, un, dun);  // frag:914-919
+                A.un = un.x;
+                B.un = un.y;
+                A.dun = dun.x;
+                B.dun = dun.y;
+                A.rB = __builtin_amdgcn_rcpf(A.un);
+                B.rB = __builtin_amdgcn_rcpf(B.un);
+                const v2f rb = {A.rB, B.rB}, ra = {A.rA, B.rA}, G = {e1.x, e1.x}, K = {e1.z, e1.z};
+                const v2f dr = rb - ra;
+                const v2f x = __builtin_elementwise_fma(dr, dr, (ra * rb) * G);
+                const v2f sq = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+                const v2f tn = __builtin_elementwise_fma(sq, K, v2f{A.T, B.T});
+                A.Tn = tn.x;
+                B.Tn = tn.y;
+                if (CM) {
+                    A.par = chord_parallel(A.cm, cda, A.rB * e.z - A.rA * pc.x, A.rB * e.w - A.rA * pc.y,
+                                           point_err(A.rA, A.rB));
+                    A.lim = A.par ? nmin(lA0, A.mh) : lA0;
+                    B.par = chord_parallel(B.cm, cdb, B.rB * e.z - B.rA * pc.x, B.rB * e.w - B.rA * pc.y,
+                                           point_err(B.rA, B.rB));
+                    B.lim = B.par ? nmin(lB0, B.mh) : lB0;
+                }
+                return __ballot(!(A.Tn < A.lim) || A.un < fr.u_f || !(B.Tn < B.lim) || B.un < fr.u_f);
+            };
+            auto apply = [&](float4 en, float4 en1) -> bool {
+                A.T = A.Tn;
+                B.T = B.Tn;
+                A.up = A.r.u;
+                B.up = B.r.u;
+                A.r.u = A.un;
+                B.r.u = B.un;
+                A.r.du = A.dun;
+                B.r.du = B.dun;
+                A.rA = A.rB;
+                B.rA = B.rB;
+                tp += 2;
+                if (CM) pc = F2(e.z, e.w);
+                e = en;
+                e1 = en1;
+                return ++i >= N;
+            };
+            for (;;) {
+                float4 nx[2 * SR_FAST_UNROLL];
+#pragma unroll
+                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
+                __builtin_amdgcn_sched_barrier(0);
+                bool leave = false;
+#pragma unroll
+                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
+                    if (compute()) {
+#pragma unroll
+                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        leave = true;
+                    } else {
+                        leave = apply(nx[2 * k], nx[2 * k + 1]);
+                    }
+                }
+                if (leave) break;
+            }
+        };
+        if (any_cm) fast(std::true_type{});
+        else fast(std::false_type{});
+        if (i >= N) break;
+        // ---- slow path of step i, per ray: exits, then step i applied, then
+        // the budget event and the exact chord (integrate's code)
+        const int steps = i + 1;
+        // a ray whose step needs nothing: apply it (no swap)
+        auto apply_plain = [&](PairRay& L) {
+            if (L.st < 0) {
+                L.T = L.Tn;
+                L.up = L.r.u;
+                L.r.u = L.un;
+                L.r.du = L.dun;
+                L.rA = L.rB;
+                L.force = false;
+            }
+        };
+        auto needs = [&](const PairRay& L) { return L.st < 0 && (L.un < 0.0f || !(L.Tn < L.lim)); };
+        if (!__ballot(needs(A))) apply_plain(A);
+        if (!__ballot(needs(B))) apply_plain(B);
+        each(needs, [&](PairRay& L, int k) {
+            if (L.st >= 0) return;
+            Budget bs = pair_budget(L, k ? EB : E0, pa0, slab0);
+            if (L.un < 0.0f) {
+                settle_prev(L, i);
+                finish(L, k, ST_BG, steps, i);
+                return;
+            }
+            const bool event = !(L.Tn < L.lim);
+            const float ahead = SR_AHEAD * (L.Tn - bs.T) + SR_AHEAD_T * L.Tn;
+            bs.T = L.Tn;
+            L.up = L.r.u;
+            L.r.u = L.un;
+            L.r.du = L.dun;
+            const float rAold = L.rA;
+            L.rA = L.rB;
+            const bool reseeded = L.force;
+            L.force = false;
+            do {
+                if (!__ballot(event)) break;
+                const f2 p1 = phi_cs(i - 1);
+                const bool exact_start = L.im == i - 1;
+                const f3 Ap = exact_start ? L.r.ro : point_near(L.r, rAold, p1.x, p1.y);
+                const f3 Bp = point_near(L.r, L.rB, e.z, e.w);
+                const float pe = point_err(exact_start ? 0.0f : rAold, L.rB);
+                if (reseeded) {
+                    const f3 dv = Bp - Ap;
+                    bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
+                }
+                const uint32_t reach = budget_event(sc, bs, Ap, Bp, pe, L.par, reseeded, ahead,
+                                                    L.r.du < 0.0f && L.r.u < 0.6f, fr.out_dip);
+                if (!__ballot(reach != 0u)) break;
+                // frag:924-930: the exact chord of step i
+                f3 prev = L.im == i - 1 ? L.r.ro : point_at(L.r, L.up, p1.x, p1.y);
+                L.r.ro = point_at(L.r, L.r.u, e.z, e.w);
+                L.im = i;
+                f3 delta = L.r.ro - prev;
+                float seg = len(delta);
+                L.r.rd = delta / seg;
+                const Hit hit = closest_hit_chord(sc, segs, reach, prev, L.r.rd, seg);
+                if (hit.slot != SLOT_NONE) {
+                    const int op = hit_opacity(sc, fr, tx, hit, -L.r.rd, false);
+                    if (op == OP_ZERO) break;
+                    if (hit.slot == SLOT_BH) {
+                        pair_store_budget(L, bs);
+                        finish(L, k, ST_BH, steps, i);
+                        return;
+                    }
+                    float* h = ps.hit(k ? idB : idA, L.n);
+                    h[0] = hit.p.x;
+                    h[1] = hit.p.y;
+                    h[2] = hit.p.z;
+                    h[3] = __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (steps << 8));
+                    h[4] = L.r.rd.x;
+                    h[5] = L.r.rd.y;
+                    h[6] = L.r.rd.z;
+                    L.n++;
+                    if (op == OP_OPAQUE || L.n == SR_PS_HITS) {
+                        pair_store_budget(L, bs);
+                        finish(L, k, op == OP_OPAQUE ? ST_HIT : ST_MORE, steps, i);
+                        return;
+                    }
+                }
+            } while (false);
+            pair_store_budget(L, bs);
+        });
+        if (A.st >= 0 && B.st >= 0) break;
+        i++;
+    }
+    // the end of the loop (frag:935): rays still alive leave towards the skybox
+    if (i >= N) {
+        if (A.st < 0) {
+            settle_prev(A, N);
+            finish(A, 0, ST_BG, N, N);
+        }
+        if (B.st < 0) {
+            settle_prev(B, N);
+            finish(B, 1, ST_BG, N, N);
+        }
+    }
+    return smax;
 }
 
 // The ray's ending (frag:874-876, 895-897, 903-905, 935) after its hits.
@@ -2021,12 +2434,9 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST>(sc, segs, tbl, fr, tx, r, hit, log);
-        ps.puti(PS_STATUS, id, st);
-        ps.puti(PS_STEPS, id, r.steps);
-        ps.puti(PS_NHITS, id, log.n);
-        ps.put3(PS_RO, id, r.ro);
-        ps.put3(PS_RD, id, r.rd);
-        if (st == ST_HIT || st == ST_MORE) {  // resumable
+        ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
+        if (st == ST_FLAT || st == ST_MORE) ps.put3(PS_RO, id, r.ro);
+        if (st == ST_MORE) {  // resumable (sr_resume_kernel)
             ps.puti(PS_I, id, r.i);
             ps.put3(PS_NV, id, r.nv);
             ps.put3(PS_TV, id, r.tv);
@@ -2098,6 +2508,81 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
         }
     }
 }
+
+#if !defined(SR_PROF) && !defined(SR_STATS)
+#ifndef SR_PAIR_WAVES_PER_EU
+#define SR_PAIR_WAVES_PER_EU 5
+#endif
+// Two rays per lane (integrate_pair): 1-D grid, workgroup s = (slot * B + f)
+// * 2 + part renders part `part` of launch code order[slot] of frame f: its
+// 64 lanes carry the rays of wave tiles `part` (A) and `part + 2` (B) of the
+// 16x16 tile, vertically adjacent 8x8 tiles. Dynamic LDS: 2 x pair_rows x 64
+// floats (the two rays' budgets). Whole tiles only (no split codes), no
+// per-wave cost map (sr_wave_costs runs sr_integrate_kernel).
+__global__ __launch_bounds__(64, SR_PAIR_WAVES_PER_EU) void sr_integrate_pair_kernel(
+    const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
+    const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
+    size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
+    extern __shared__ float lds_pair[];
+    const unsigned B = (unsigned)fr.batch;
+    const unsigned bid = blockIdx.x;
+    const unsigned wg = bid >> 1;  // the tile's workgroup index (slot * B + f)
+    const int frame = B > 1 ? (int)(wg % B) : 0;
+    const unsigned slot = B > 1 ? wg / B : wg;
+    const int code = order ? order[slot] : ((int)slot << 8);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
+    if (code < 0 || (code & SR_SPLIT)) return;
+    const int block = code >> 8;
+    if (order && wg < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
+    const int part = (int)(bid & 1u);
+    const int tA = part * 64 + (int)threadIdx.x, tB = tA + 128;
+    const size_t base = ((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256;
+    const PS ps{ps_base, ps_n};
+    Tex tx;
+    tx.bg = nullptr;
+    tx.arr = arr;
+    tx.opq = opq;
+    const int nb = sc->num_budget, ncyl = __builtin_popcount((unsigned)sc->budget_cyl_mask);
+    const int rows = SR_PAIR_ROWS(nb, ncyl);
+    float* const E0 = lds_pair + threadIdx.x;
+    PairRay A, Bq;
+    // camera ray (frag:859-889) of one ray; rays that end at once (flat, noise
+    // mask) write their record; off-frame threads do nothing
+    auto init = [&](PairRay& L, int t, float* E) {
+        L.n = 0;
+        L.force = false;
+        L.im = -1;
+        L.up = 0.0f;
+        L.T = 0.0f;
+        L.m = L.mh = INFINITY;
+        L.cm = 0u;
+        L.st = ST_DONE;
+        L.r.u = 2.0f / 3.0f;
+        L.r.du = 0.0f;
+        Pix q;
+        if (!pixel_of(fr, block, t, q)) return;  // parked, no record
+        const int st = init_pixel(fr, fr.cam[frame], q, L.r);
+        if (st >= 0) {
+            pair_finish(ps, base + t, L, st, 0, 0);
+            return;
+        }
+        L.st = -1;
+        Budget bs = pair_budget(L, E, nb + 1, nb + 1 + 2 * ncyl);
+        budget_init(sc, bs, L.r.ro, L.r.nv, L.r.tv, L.r.du < 0.0f && L.r.u < 0.6f, fr.out_dip);
+        pair_store_budget(L, bs);
+        L.rA = __builtin_amdgcn_rcpf(L.r.u);
+    };
+    init(A, tA, E0);
+    init(Bq, tB, E0 + (size_t)rows * SR_E_STRIDE);
+    int steps = 0;
+    if (A.st < 0 || Bq.st < 0) steps = integrate_pair(sc, segs, tbl, fr, tx, ps, base + tA, base + tB, E0, A, Bq);
+    if (cost) {  // all 64 lanes are active here
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
+        if ((threadIdx.x & 63) == 0) atomicMax(&cost[block], steps);
+    }
+}
+#endif
 
 // Launch order for the next frame: workgroup tiles by descending cost of this
 // frame (counting sort on 256 cost buckets), so the long rays - those
@@ -2176,34 +2661,45 @@ __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __res
     tx.bg = bg;
     tx.arr = arr;
     tx.opq = nullptr;
-    const int st = ps.geti(PS_STATUS, id);
-    const int nh = ps.geti(PS_NHITS, id);
+    const float4 rec = ps.get_rec(id);
+    const int w0 = __float_as_int(rec.x);
+    const int st = w0 & 7, nh = (w0 >> 3) & 7;
     f4 frag = crosshair_frag(fr, q);
     bool done = false;
     int steps_at = -1;
     for (int j = 0; j < nh && !done; j++) {  // frag:930-932 for each recorded hit, in order
-        const int f = PS_HIT0 + PS_HIT_STRIDE * j;
+        const float4* h4 = reinterpret_cast<const float4*>(ps.hit(id, j));
+        const float4 a = h4[0], b = h4[1];
         Hit h = no_hit();
-        h.p = ps.get3(f, id);
-        const int key = ps.geti(f + 3, id);
+        const int hw = __float_as_int(a.w);
+        const int key = (hw & 0xff) - PS_KEY_BIAS;
         h.slot = key >> 3;
         h.face = key & 7;
-        f4 c = shade(sc, fr, tx, h, -ps.get3(f + 4, id));
+        h.p = F3(a.x, a.y, a.z);
+        f4 c = shade(sc, fr, tx, h, -F3(b.x, b.y, b.z));
         frag = frag + c;
         done = c.w == 1.0f;
-        if (done) steps_at = ps.geti(f + 7, id);
+        if (done) steps_at = (int)((unsigned)hw >> 8);
+    }
+    if (!done && st == ST_BH) {  // the ray's end in the black hole: vec4(0, 0, 0, 1) (shade_hit)
+        frag = frag + F4(0.0f, 0.0f, 0.0f, 1.0f);
+        done = true;
+        steps_at = (int)((unsigned)w0 >> 8);
     }
     if (!done) {
-        if (st == ST_HIT || st == ST_MORE) {
-            // every hit so far translucent, the ray stopped early: accumulate
-            // and queue for sr_resume_kernel
+        if (st == ST_MORE) {
+            // every hit so far translucent, the ray stopped with its log
+            // full: accumulate and queue for sr_resume_kernel (an ST_HIT
+            // pixel ends at its last hit, opaque exactly: done above)
             ps.put4(PS_FRAG, id, frag);
             list[atomicAdd(count, 1)] = (int)id;
             return;
         }
-        finish_ray(sc, segs, fr, tx, st, ps.get3(PS_RO, id), ps.get3(PS_RD, id), frag);
+        if (st == ST_FLAT || st == ST_BG)  // ro only for the flat intersect
+            finish_ray(sc, segs, fr, tx, st, st == ST_FLAT ? ps.get3(PS_RO, id) : F3(0.0f, 0.0f, 0.0f),
+                       F3(rec.y, rec.z, rec.w), frag);
     }
-    if (dbg_steps && steps_at < 0) steps_at = ps.geti(PS_STEPS, id);
+    if (dbg_steps && steps_at < 0) steps_at = (int)((unsigned)w0 >> 8);
     write_pixel(fr, out, pitch, dbg_rgba, dbg_steps, q, frag, steps_at);
 }
 
@@ -2230,14 +2726,15 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         pixel_of(fr, (id >> 8) - f * fr.tiles, id & 255, q);
         Ray r;
         f4 frag = ps.get4(PS_FRAG, id);
+        const float4 rec = ps.get_rec(id);
         r.ro = ps.get3(PS_RO, id);
-        r.rd = ps.get3(PS_RD, id);
+        r.rd = F3(rec.y, rec.z, rec.w);
         r.nv = ps.get3(PS_NV, id);
         r.tv = ps.get3(PS_TV, id);
         r.u = ps.at(PS_U, id);
         r.du = ps.at(PS_DU, id);
         r.i = ps.geti(PS_I, id) + 1;
-        r.steps = ps.geti(PS_STEPS, id);
+        r.steps = (int)((unsigned)__float_as_int(rec.x) >> 8);
         HitLog log{ps, (size_t)id, 0};
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();
@@ -2281,6 +2778,13 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
+#if !defined(SR_PROF) && !defined(SR_STATS)
+    if (fr->pair && cull && !fr->wave_cost && !split) {
+        const size_t lds = 2u * (size_t)fr->pair_rows * SR_E_STRIDE * sizeof(float);
+        hipLaunchKernelGGL(sr_integrate_pair_kernel, dim3(slots * B * 2), dim3(64), lds, stream, sc, tbl, segs, arr,
+                           opq, *fr, ps, ps_n, count, order, cost);
+    } else
+#endif
     if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);

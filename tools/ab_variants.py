@@ -29,6 +29,12 @@ def main():
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--camera", default="default")
     ap.add_argument("--scene", choices=["tex", "untex", "bh"], default="tex")
+    ap.add_argument("--throughput", action="store_true",
+                    help="bench.py's pipeline instead of single frames: --frames frames in launches of --batch "
+                         "(sr_render_blocks_batch), --inflight launches in flight on their own contexts and streams")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--inflight", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=48)
     args = ap.parse_args()
     import torch
 
@@ -74,6 +80,53 @@ def main():
                                       C.c_void_p(st.data_ptr()), sp), "debug")
         torch.cuda.synchronize()
         nsteps[name] = int(st.sum().item())
+    if args.throughput:
+        # per variant: inflight contexts, each with its stream and a B-frame output
+        tp = []
+        for name, lib, ctx0, _ in variants:
+            ctxs = []
+            for k in range(args.inflight):
+                c = ctx0
+                if k:
+                    c = C.c_void_p()
+                    abi.check(lib.sr_create(C.byref(c), 0), "sr_create")
+                    abi.check(lib.sr_set_scene(c, C.byref(scene)), "scene")
+                    abi.check(lib.sr_set_background(c, bg.ctypes.data, bg.shape[1], bg.shape[0], 3), "bg")
+                    abi.check(lib.sr_set_texture_array(c, arr.ctypes.data, arr.shape[2], arr.shape[1], arr.shape[0],
+                                                       arr.shape[3]), "arr")
+                st = torch.cuda.Stream()
+                o = torch.empty((args.batch, H, W, 4), dtype=torch.uint8, device="cuda")
+                ctxs.append((c, st, o))
+            tp.append((name, lib, ctxs))
+        cams = (abi.Camera * args.batch)(*([cam] * args.batch))
+
+        def run_tp(v):
+            _, lib, ctxs = v
+            for j in range(args.frames // args.batch):
+                c, st, o = ctxs[j % len(ctxs)]
+                abi.check(lib.sr_render_blocks_batch(c, cams, args.batch, C.byref(params), W, H, 8, 0, 1,
+                                                     C.c_void_p(o.data_ptr()), W * 4, o[0].numel(),
+                                                     C.c_void_p(st.cuda_stream)), "batch")
+            torch.cuda.synchronize()
+
+        for v in tp:
+            run_tp(v)  # learn the launch orders
+        ttimes = {v[0]: [] for v in tp}
+        import time
+        for _ in range(args.rounds):
+            for v in tp:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                run_tp(v)
+                ttimes[v[0]].append((time.perf_counter() - t0) * 1e3 / args.frames)
+        tref = tp[0][2][0][2].cpu().numpy()
+        res = {k: {"median_ms_per_frame": float(np.median(t)), "min_ms_per_frame": float(np.min(t)),
+                   "mpix_s": W * H / (np.median(t) * 1e-3) / 1e6,
+                   "identical": bool(np.array_equal(dict((v[0], v) for v in tp)[k][2][0][2].cpu().numpy(), tref))}
+               for k, t in ttimes.items()}
+        print(json.dumps({"throughput": res, "batch": args.batch, "inflight": args.inflight, "frames": args.frames},
+                         indent=1))
+        return
     ref = variants[0][3].cpu().numpy()
     same = {v[0]: bool(np.array_equal(v[3].cpu().numpy(), ref)) for v in variants}
     times = {v[0]: [] for v in variants}

@@ -98,7 +98,70 @@ __global__ __launch_bounds__(64) void kern(const float4* __restrict__ tbl, int n
     if (threadIdx.x == 0 && n < 0) pad[0] = 1.0f;
 }
 
+// The production fast loop's shape (kernels/geodesic.hip integrate): three
+// steps per iteration, the next three steps' table entries loaded together at
+// the iteration's top, an exit ballot per step.
 template <int RAYS>
+__global__ __launch_bounds__(64) void kern3(const float4* __restrict__ tbl, int n, float* out) {
+    extern __shared__ float pad[];
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    const float lim = 1e30f, uf = 0.01f;
+    int exits = 0;
+    const cf4* tp = (const cf4*)tbl;
+    sr_v4f e = tp[0], e1 = tp[1];
+    v2f u, du, rA, T;
+    if (RAYS == 1) {
+        u = {0.3f + (t & 1023) * 1e-5f, 0.0f};
+        du = {0.01f, 0.0f};
+    } else {
+        u = {0.3f + (t & 1023) * 1e-5f, 0.31f + (t & 1023) * 1e-5f};
+        du = {0.01f, 0.012f};
+    }
+    rA = {1.0f / u.x, 1.0f / u.y};
+    T = {0.0f, 0.0f};
+    for (int i = 0; i < n; i += 3) {
+        sr_v4f nx[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) nx[k] = tp[2 + k];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            v2f un, dun, rB, Tn;
+            if (RAYS == 1) {
+                float a, b;
+                rk4_1(u.x, du.x, e.x, e1.y, e.y, a, b);
+                un = {a, 0.0f};
+                dun = {b, 0.0f};
+                const float r = __builtin_amdgcn_rcpf(a);
+                const float dr = r - rA.x;
+                const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA.x * r) * e1.x));
+                rB = {r, 0.0f};
+                Tn = {__builtin_fmaf(sq, e1.z, T.x), 0.0f};
+                if (__ballot(!(Tn.x < lim) || a < uf)) exits++;
+            } else {
+                rk4_2(u, du, e.x, e1.y, e.y, un, dun);
+                rB = {__builtin_amdgcn_rcpf(un.x), __builtin_amdgcn_rcpf(un.y)};
+                const v2f dr = rB - rA;
+                const v2f G = {e1.x, e1.x}, K = {e1.z, e1.z};
+                const v2f x = __builtin_elementwise_fma(dr, dr, (rA * rB) * G);
+                const v2f sq = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+                Tn = __builtin_elementwise_fma(sq, K, T);
+                if (__ballot(!(Tn.x < lim) || un.x < uf || !(Tn.y < lim) || un.y < uf)) exits++;
+            }
+            T = Tn;
+            u = un;
+            du = dun;
+            rA = rB;
+            e = nx[2 * k];
+            e1 = nx[2 * k + 1];
+        }
+        tp += 6;
+    }
+    out[t] = u.x + u.y + du.x + du.y + T.x + T.y + exits;
+    if (threadIdx.x == 0 && n < 0) pad[0] = 1.0f;
+}
+
+template <int RAYS, bool THREE>
 double run(const float4* tbl, int n, float* out, int waves_per_simd, int cus) {
     const int blocks = cus * 4 * waves_per_simd * 4;  // 4 rounds of full occupancy
     const size_t lds = (160 * 1024) / (4 * waves_per_simd) - 256;
@@ -108,7 +171,8 @@ double run(const float4* tbl, int n, float* out, int waves_per_simd, int cus) {
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
         (void)hipEventRecord(a, 0);
-        hipLaunchKernelGGL(kern<RAYS>, dim3(blocks), dim3(64), lds, 0, tbl, n, out);
+        if (THREE) hipLaunchKernelGGL(kern3<RAYS>, dim3(blocks), dim3(64), lds, 0, tbl, n, out);
+        else hipLaunchKernelGGL(kern<RAYS>, dim3(blocks), dim3(64), lds, 0, tbl, n, out);
         (void)hipEventRecord(b, 0);
         (void)hipEventSynchronize(b);
         float ms = 0;
@@ -126,21 +190,23 @@ int main(int argc, char** argv) {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, 0);
     const int cus = prop.multiProcessorCount;
-    (void)hipMalloc(&tbl, sizeof(float4) * 2 * (n + 4));
-    float4* h = new float4[2 * (n + 4)];
-    for (int i = 0; i < n + 4; i++) {
+    (void)hipMalloc(&tbl, sizeof(float4) * 2 * (n + 8));
+    float4* h = new float4[2 * (n + 8)];
+    for (int i = 0; i < n + 8; i++) {
         const float s = 12.566371f / n;
         h[2 * i] = make_float4(s, s / 6, 0.5f, 0.5f);
         h[2 * i + 1] = make_float4(1e-5f, 0.5f * s, 1.0102f, 0.0f);
     }
-    (void)hipMemcpy(tbl, h, sizeof(float4) * 2 * (n + 4), hipMemcpyHostToDevice);
+    (void)hipMemcpy(tbl, h, sizeof(float4) * 2 * (n + 8), hipMemcpyHostToDevice);
     (void)hipMalloc(&out, (size_t)cus * 4 * 8 * 4 * 64 * sizeof(float));
     printf("{\"cus\": %d, \"steps\": %d, \"results\": [", cus, n);
     bool first = true;
     for (int w : {2, 3, 4, 5, 6, 8}) {
-        const double one = run<1>(tbl, n, out, w, cus), two = run<2>(tbl, n, out, w, cus);
-        printf("%s{\"waves_per_simd\": %d, \"one_ray_Tsteps\": %.4f, \"two_rays_Tsteps\": %.4f}", first ? "" : ", ", w,
-               one, two);
+        const double one = run<1, false>(tbl, n, out, w, cus), two = run<2, false>(tbl, n, out, w, cus);
+        const double one3 = run<1, true>(tbl, n, out, w, cus), two3 = run<2, true>(tbl, n, out, w, cus);
+        printf("%s{\"waves_per_simd\": %d, \"one_ray_Tsteps\": %.4f, \"two_rays_Tsteps\": %.4f, "
+               "\"one_ray_3step_prefetch_Tsteps\": %.4f, \"two_rays_3step_prefetch_Tsteps\": %.4f}",
+               first ? "" : ", ", w, one, two, one3, two3);
         first = false;
     }
     printf("]}\n");
