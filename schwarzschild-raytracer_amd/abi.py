@@ -203,7 +203,6 @@ SIGNATURES = {
 # exported beside the header set (parity tooling)
 EXTRA_SIGNATURES = {
     "sr_debug_set_culling": (_i, [_p, _i]),
-    "sr_debug_set_pair": (_i, [_p, _i]),
     "sr_debug_set_timing": (_i, [_p, _i]),
     "sr_debug_kernel_times": (_i, [_p, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
     "sr_debug_last_order": (_i, [_p, C.POINTER(_i), _i, C.POINTER(_i)]),

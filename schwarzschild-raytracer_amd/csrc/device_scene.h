@@ -184,11 +184,6 @@ typedef struct {
     int32_t split_tiles;
     int32_t split_log2;
     int32_t split_min_steps;
-    // two rays per lane (sr_integrate_pair_kernel): on, and the LDS rows per
-    // ray of the packed budget layout (1 + budget slots + 3 x budgeted
-    // cylinders, at least SR_MAX_BUDGET + 1)
-    int32_t pair;
-    int32_t pair_rows;
 } sr_dev_frame;
 
 #endif

@@ -545,6 +545,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #ifndef SR_AHEAD_T
 #define SR_AHEAD_T 1.0f
 #endif
+#ifndef SR_COAST  // the RK4-only fast loop of waves whose every budget is +inf (integrate)
+#define SR_COAST 1
+#endif
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
 #define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
@@ -554,8 +557,7 @@ struct Budget {
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
     float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
                   // covers chords nearly parallel to an axis
-    int pa0, slab0;  // LDS rows of pa[0] and H[0]: SR_E_PA0 / SR_E_SLAB0 (static layout), or packed
-                     // after the scene's budget slots (sr_integrate_pair_kernel)
+    int pa0, slab0;  // LDS rows of pa[0] and H[0] (SR_E_PA0 / SR_E_SLAB0)
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -1808,7 +1810,54 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (leave) break;
             }
         };
+        // Coasting: when every lane's limit is +inf (escaping rays that have
+        // passed every object: outward_clear gave all their budgets +inf),
+        // nothing but u < u_f (or the end of the loop) can stop a lane until
+        // its next event or reseed, which re-anchors every slot: a step is
+        // RK4 and that compare. The chord bound and its path T are skipped
+        // (T is reset at that re-anchor; rB is restored on the way out), so
+        // the iterates are the same. Only outward lanes (u < 0.6 falling)
+        // coast: u stays finite.
+        auto coast = [&]() {
+            e = ldc(tp);
+            float4 e1 = ldc(tp + 1);
+            for (;;) {
+                float4 nx[2 * SR_FAST_UNROLL];
+#pragma unroll
+                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
+                __builtin_amdgcn_sched_barrier(0);
+                bool leave = false;
+#pragma unroll
+                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
+                    rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
+                    SR_STAT(0, 1);
+                    SR_STAT(11, 1);  // coasting wave-steps
+                    SR_STAT(13, __popcll(__ballot(1)));
+                    if (__ballot(un < fr.u_f)) {
+#pragma unroll
+                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        leave = true;
+                    } else {
+                        up = r.u;
+                        r.u = un;
+                        r.du = dun;
+                        tp += 2;
+                        e = nx[2 * k];
+                        e1 = nx[2 * k + 1];
+                        leave = ++i >= N;
+                    }
+                }
+                if (leave) break;
+            }
+            // the state the full loop leaves: step i's radius, no charge (every budget is +inf)
+            rA = __builtin_amdgcn_rcpf(r.u);
+            rB = __builtin_amdgcn_rcpf(un);
+            Tn = bs.T;
+            lim = lim0;
+            par = 0;
+        };
         if (any_cm) fast(std::true_type{});
+        else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
         else fast(std::false_type{});
         SR_PT(0);
         if (i >= N) break;
@@ -1944,371 +1993,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     r.steps = sbase + N;
     settle_prev(N);
     return ST_BG;
-}
-
-// ---- two rays per lane (sr_integrate_pair_kernel) ------------------------------
-// The fast loop is bound by one wave's dependency chain: RK4 (~21 dependent
-// VALU), the radius reciprocal, the chord bound's square root, the compare and
-// the exit branch, which six waves per SIMD do not hide. Here
-// each lane carries two rays - the pixels of two vertically adjacent 8x8 wave
-// tiles - that share the wave-uniform step index and step-table loads: their
-// RK4s run as packed pairs ACROSS the rays ((uA, uB), (u'A, u'B): the same
-// IEEE operations per ray as rk4_step, so bit-identical), two independent
-// chains per lane in ~1.4x the instructions of one.
-// Each ray keeps its own state and clearance budgets (its own LDS columns);
-// the slow path is one copy of the single-ray code run for ray A, then - with
-// the two rays' registers swapped - for ray B, only for a ray set in which
-// some lane needs attention. A ray that ends writes its pixel record and
-// parks on the circular photon orbit (u = 2/3 exactly, u' = 0: ddu = -0, so
-// RK4 leaves it fixed) with an infinite limit, so it never triggers an exit.
-// Every per-ray decision is the single-ray kernel's (each ray's budget events
-// are those of its own 64-ray set), so pixels are bit-identical to it.
-// LDS rows per ray: E[0..nb], pa/pb and H of the budgeted cylinders; at least
-// the 9 rows budget_event reads unconditionally
-#define SR_PAIR_ROWS(nb, ncyl) (1 + (nb) + 3 * (ncyl) > SR_MAX_BUDGET + 1 ? 1 + (nb) + 3 * (ncyl) : SR_MAX_BUDGET + 1)
-struct PairRay {
-    Ray r;                  // ro, rd, nv, tv, u, du (the step index is the wave's)
-    float T, m, mh;         // Budget scalars
-    uint32_t cm;
-    float up, rA;           // chord bookkeeping (integrate)
-    int im;
-    int st;                 // -1 while alive, else its status (the pixel record is written)
-    int n;                  // logged hits
-    bool force;
-    float un, dun, rB, Tn, lim;  // step i as the fast loop left it
-    uint32_t par;
-};
-
-__device__ __forceinline__ void swap_rays(PairRay& a, PairRay& b) {
-    PairRay t = a;
-    a = b;
-    b = t;
-}
-
-__device__ __forceinline__ void rk4_pair(v2f u, v2f du, float h, float hh, float h6, v2f& un, v2f& dun) {
-    const v2f H1 = {h, h}, H2 = {hh, hh}, HS = {h6, h6}, two = {2.0f, 2.0f}, k15 = {1.5f, 1.5f}, one = {1.0f, 1.0f};
-    auto ddu2 = [&](v2f x) { return -x * (one - k15 * x); };
-    const v2f k1 = du, l1 = ddu2(u);
-    const v2f k2 = du + l1 * H2, l2 = ddu2(u + k1 * H2);
-    const v2f k3 = du + l2 * H2, l3 = ddu2(u + k2 * H2);
-    const v2f k4 = du + l3 * H1, l4 = ddu2(u + k3 * H1);
-    un = u + HS * (__builtin_elementwise_fma(two, k3, __builtin_elementwise_fma(two, k2, k1)) + k4);
-    dun = du + HS * (__builtin_elementwise_fma(two, l3, __builtin_elementwise_fma(two, l2, l1)) + l4);
-}
-
-// The pixel record of a ray that has ended (sr_integrate_kernel's hand-off).
-__device__ __forceinline__ void pair_finish(const PS& ps, size_t id, PairRay& L, int st, int steps, int i) {
-    ps.put_rec(id, ps_word(st, L.n, steps), L.r.rd);
-    if (st == ST_FLAT || st == ST_MORE) ps.put3(PS_RO, id, L.r.ro);
-    if (st == ST_MORE) {
-        ps.puti(PS_I, id, i);
-        ps.put3(PS_NV, id, L.r.nv);
-        ps.put3(PS_TV, id, L.r.tv);
-        ps.at(PS_U, id) = L.r.u;
-        ps.at(PS_DU, id) = L.r.du;
-    }
-    L.st = st;
-    L.r.u = 2.0f / 3.0f;  // the circular photon orbit: ddu(u) = -0, RK4 keeps it
-    L.r.du = 0.0f;
-    L.m = INFINITY;
-    L.mh = INFINITY;
-    L.cm = 0u;
-    L.force = false;
-}
-
-// Budget views of a PairRay (the single-ray helpers take a Budget); E: the
-// ray's LDS columns, rows packed after the scene's budget slots
-__device__ __forceinline__ Budget pair_budget(const PairRay& L, float* E, int pa0, int slab0) {
-    Budget bs;
-    bs.E = E;
-    bs.pa0 = pa0;
-    bs.slab0 = slab0;
-    bs.T = L.T;
-    bs.m = L.m;
-    bs.mh = L.mh;
-    bs.cm = L.cm;
-    return bs;
-}
-__device__ __forceinline__ void pair_store_budget(PairRay& L, const Budget& bs) {
-    L.T = bs.T;
-    L.m = bs.m;
-    L.mh = bs.mh;
-    L.cm = bs.cm;
-}
-
-// Both rays of every lane from step 0 (sr_integrate_pair_kernel): A = ray
-// slot 0, B = slot 1; alive rays have passed init_pixel. Writes the pixel
-// records; returns the lane's largest step count.
-__device__ __forceinline__ int integrate_pair(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
-                                              const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
-                                              const PS& ps, size_t idA, size_t idB, float* E0, PairRay& A,
-                                              PairRay& B) {
-    const int N = fr.max_steps;
-    const int nb = sc->num_budget, ncyl = __builtin_popcount((unsigned)sc->budget_cyl_mask);
-    const int rows = SR_PAIR_ROWS(nb, ncyl);
-    const int pa0 = nb + 1, slab0 = nb + 1 + 2 * ncyl;
-    float* const EB = E0 + (size_t)rows * SR_E_STRIDE;  // ray B's columns
-    int smax = 0;
-    auto phi_cs = [&](int j) -> f2 {
-        if (j < 0) return F2(1.0f, 0.0f);
-        const float4 t = tbl[2 * j];
-        return F2(t.z, t.w);
-    };
-    // materialise ray L's chord of step i - 1
-    auto settle_prev = [&](PairRay& L, int i) {
-        if (L.im == i - 1) return;
-        const f2 p1 = phi_cs(i - 1);
-        f3 Aq;
-        if (L.im == i - 2) {
-            Aq = L.r.ro;
-        } else {
-            const f2 p2 = phi_cs(i - 2);
-            Aq = point_at(L.r, L.up, p2.x, p2.y);
-        }
-        f3 Bq = point_at(L.r, L.r.u, p1.x, p1.y);
-        f3 delta = Bq - Aq;
-        float seg = len(delta);
-        L.r.rd = delta / seg;
-        L.r.ro = Bq;
-        L.im = i - 1;
-    };
-    auto finish = [&](PairRay& L, int k, int st, int steps, int i) {
-        pair_finish(ps, k ? idB : idA, L, st, steps, i);
-        smax = max(smax, steps);
-    };
-    // One copy of a per-ray body for ray A, then for ray B with the two rays'
-    // registers swapped (f(L, k): L is the current ray, k its slot); a set in
-    // which no lane's `need` holds is skipped.
-#ifdef SR_PAIR_SWAP
-    auto each = [&](auto need, auto f) {
-#pragma clang loop unroll(disable)
-        for (int k = 0; k < 2; k++) {
-            if (k == 1) {
-                if (!__ballot(need(B))) break;
-                swap_rays(A, B);
-            } else if (!__ballot(need(A))) {
-                continue;
-            }
-            f(A, k);
-            if (k == 1) swap_rays(A, B);
-        }
-    };
-#else
-    auto each = [&](auto need, auto f) {
-        if (__ballot(need(A))) f(A, 0);
-        if (__ballot(need(B))) f(B, 1);
-    };
-#endif
-    int i = 0;
-    for (;;) {
-        i = __builtin_amdgcn_readfirstlane(i);
-        if (i >= N) break;
-        // frag:891-912 at the top of step i, per ray
-        each([&](const PairRay& L) { return L.st < 0 && L.r.u < fr.u_f; },
-             [&](PairRay& L, int k) {
-                 if (L.st < 0 && L.r.u < fr.u_f) {
-                     settle_prev(L, i);
-                     f3 q;
-                     if (!sphere_test(L.r.ro, L.r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) {
-                         finish(L, k, ST_FLAT, i + 1, i);
-                         return;
-                     }
-                     L.r.nv = nrm(q);
-                     if (fabsf(dot(L.r.rd, L.r.nv)) >= 1.0f - SR_EPS) {
-                         finish(L, k, ST_FLAT, i + 1, i);
-                         return;
-                     }
-                     L.r.tv = nrm(cross(cross(L.r.nv, L.r.rd), L.r.nv));
-                     L.r.u = 1.0f / len(q);
-                     L.r.du = -L.r.u * dot(L.r.rd, L.r.nv) / dot(L.r.rd, L.r.tv);
-                     Budget bs = pair_budget(L, k ? EB : E0, pa0, slab0);
-                     budget_frame(sc, bs, L.r.nv, L.r.tv);
-                     pair_store_budget(L, bs);
-                     L.force = true;
-                 }
-             });
-        if (A.st >= 0 && B.st >= 0) break;  // both rays of this lane have ended
-        // ---- fast loop over both rays (see integrate)
-        const float lA0 = A.st >= 0 ? INFINITY : (A.force ? -INFINITY : A.m);
-        const float lB0 = B.st >= 0 ? INFINITY : (B.force ? -INFINITY : B.m);
-        const bool any_cm = __ballot((A.cm | B.cm) != 0u);
-        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
-        float4 e;
-        auto fast = [&](auto cm_tag) {
-            constexpr bool CM = decltype(cm_tag)::value;
-            A.lim = lA0;
-            B.lim = lB0;
-            A.par = B.par = 0;
-            e = ldc(tp);
-            float4 e1 = ldc(tp + 1);
-            f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);
-            Budget ba = pair_budget(A, E0, pa0, slab0), bb = pair_budget(B, EB, pa0, slab0);
-            const CylDirs cda = CM ? cyl_dirs(sc, ba) : CylDirs{};
-            const CylDirs cdb = CM ? cyl_dirs(sc, bb) : CylDirs{};
-            if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-            auto compute = [&]() -> bool {
-                v2f un, dun;
-                rk4_pair(v2f{A.r.u, B.r.u}, v2f{A.r.du, B.r.du}, e.x, e1.y, e.y, un, dun);  // frag:914-919
-                A.un = un.x;
-                B.un = un.y;
-                A.dun = dun.x;
-                B.dun = dun.y;
-                A.rB = __builtin_amdgcn_rcpf(A.un);
-                B.rB = __builtin_amdgcn_rcpf(B.un);
-                const v2f rb = {A.rB, B.rB}, ra = {A.rA, B.rA}, G = {e1.x, e1.x}, K = {e1.z, e1.z};
-                const v2f dr = rb - ra;
-                const v2f x = __builtin_elementwise_fma(dr, dr, (ra * rb) * G);
-                const v2f sq = {__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
-                const v2f tn = __builtin_elementwise_fma(sq, K, v2f{A.T, B.T});
-                A.Tn = tn.x;
-                B.Tn = tn.y;
-                if (CM) {
-                    A.par = chord_parallel(A.cm, cda, A.rB * e.z - A.rA * pc.x, A.rB * e.w - A.rA * pc.y,
-                                           point_err(A.rA, A.rB));
-                    A.lim = A.par ? nmin(lA0, A.mh) : lA0;
-                    B.par = chord_parallel(B.cm, cdb, B.rB * e.z - B.rA * pc.x, B.rB * e.w - B.rA * pc.y,
-                                           point_err(B.rA, B.rB));
-                    B.lim = B.par ? nmin(lB0, B.mh) : lB0;
-                }
-                return __ballot(!(A.Tn < A.lim) || A.un < fr.u_f || !(B.Tn < B.lim) || B.un < fr.u_f);
-            };
-            auto apply = [&](float4 en, float4 en1) -> bool {
-                A.T = A.Tn;
-                B.T = B.Tn;
-                A.up = A.r.u;
-                B.up = B.r.u;
-                A.r.u = A.un;
-                B.r.u = B.un;
-                A.r.du = A.dun;
-                B.r.du = B.dun;
-                A.rA = A.rB;
-                B.rA = B.rB;
-                tp += 2;
-                if (CM) pc = F2(e.z, e.w);
-                e = en;
-                e1 = en1;
-                return ++i >= N;
-            };
-            for (;;) {
-                float4 nx[2 * SR_FAST_UNROLL];
-#pragma unroll
-                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
-                __builtin_amdgcn_sched_barrier(0);
-                bool leave = false;
-#pragma unroll
-                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
-                    if (compute()) {
-#pragma unroll
-                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
-                        leave = true;
-                    } else {
-                        leave = apply(nx[2 * k], nx[2 * k + 1]);
-                    }
-                }
-                if (leave) break;
-            }
-        };
-        if (any_cm) fast(std::true_type{});
-        else fast(std::false_type{});
-        if (i >= N) break;
-        // ---- slow path of step i, per ray: exits, then step i applied, then
-        // the budget event and the exact chord (integrate's code)
-        const int steps = i + 1;
-        // a ray whose step needs nothing: apply it (no swap)
-        auto apply_plain = [&](PairRay& L) {
-            if (L.st < 0) {
-                L.T = L.Tn;
-                L.up = L.r.u;
-                L.r.u = L.un;
-                L.r.du = L.dun;
-                L.rA = L.rB;
-                L.force = false;
-            }
-        };
-        auto needs = [&](const PairRay& L) { return L.st < 0 && (L.un < 0.0f || !(L.Tn < L.lim)); };
-        if (!__ballot(needs(A))) apply_plain(A);
-        if (!__ballot(needs(B))) apply_plain(B);
-        each(needs, [&](PairRay& L, int k) {
-            if (L.st >= 0) return;
-            Budget bs = pair_budget(L, k ? EB : E0, pa0, slab0);
-            if (L.un < 0.0f) {
-                settle_prev(L, i);
-                finish(L, k, ST_BG, steps, i);
-                return;
-            }
-            const bool event = !(L.Tn < L.lim);
-            const float ahead = SR_AHEAD * (L.Tn - bs.T) + SR_AHEAD_T * L.Tn;
-            bs.T = L.Tn;
-            L.up = L.r.u;
-            L.r.u = L.un;
-            L.r.du = L.dun;
-            const float rAold = L.rA;
-            L.rA = L.rB;
-            const bool reseeded = L.force;
-            L.force = false;
-            do {
-                if (!__ballot(event)) break;
-                const f2 p1 = phi_cs(i - 1);
-                const bool exact_start = L.im == i - 1;
-                const f3 Ap = exact_start ? L.r.ro : point_near(L.r, rAold, p1.x, p1.y);
-                const f3 Bp = point_near(L.r, L.rB, e.z, e.w);
-                const float pe = point_err(exact_start ? 0.0f : rAold, L.rB);
-                if (reseeded) {
-                    const f3 dv = Bp - Ap;
-                    bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
-                }
-                const uint32_t reach = budget_event(sc, bs, Ap, Bp, pe, L.par, reseeded, ahead,
-                                                    L.r.du < 0.0f && L.r.u < 0.6f, fr.out_dip);
-                if (!__ballot(reach != 0u)) break;
-                // frag:924-930: the exact chord of step i
-                f3 prev = L.im == i - 1 ? L.r.ro : point_at(L.r, L.up, p1.x, p1.y);
-                L.r.ro = point_at(L.r, L.r.u, e.z, e.w);
-                L.im = i;
-                f3 delta = L.r.ro - prev;
-                float seg = len(delta);
-                L.r.rd = delta / seg;
-                const Hit hit = closest_hit_chord(sc, segs, reach, prev, L.r.rd, seg);
-                if (hit.slot != SLOT_NONE) {
-                    const int op = hit_opacity(sc, fr, tx, hit, -L.r.rd, false);
-                    if (op == OP_ZERO) break;
-                    if (hit.slot == SLOT_BH) {
-                        pair_store_budget(L, bs);
-                        finish(L, k, ST_BH, steps, i);
-                        return;
-                    }
-                    float* h = ps.hit(k ? idB : idA, L.n);
-                    h[0] = hit.p.x;
-                    h[1] = hit.p.y;
-                    h[2] = hit.p.z;
-                    h[3] = __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (steps << 8));
-                    h[4] = L.r.rd.x;
-                    h[5] = L.r.rd.y;
-                    h[6] = L.r.rd.z;
-                    L.n++;
-                    if (op == OP_OPAQUE || L.n == SR_PS_HITS) {
-                        pair_store_budget(L, bs);
-                        finish(L, k, op == OP_OPAQUE ? ST_HIT : ST_MORE, steps, i);
-                        return;
-                    }
-                }
-            } while (false);
-            pair_store_budget(L, bs);
-        });
-        if (A.st >= 0 && B.st >= 0) break;
-        i++;
-    }
-    // the end of the loop (frag:935): rays still alive leave towards the skybox
-    if (i >= N) {
-        if (A.st < 0) {
-            settle_prev(A, N);
-            finish(A, 0, ST_BG, N, N);
-        }
-        if (B.st < 0) {
-            settle_prev(B, N);
-            finish(B, 1, ST_BG, N, N);
-        }
-    }
-    return smax;
 }
 
 // The ray's ending (frag:874-876, 895-897, 903-905, 935) after its hits.
@@ -2509,81 +2193,6 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
     }
 }
 
-#if !defined(SR_PROF) && !defined(SR_STATS)
-#ifndef SR_PAIR_WAVES_PER_EU
-#define SR_PAIR_WAVES_PER_EU 5
-#endif
-// Two rays per lane (integrate_pair): 1-D grid, workgroup s = (slot * B + f)
-// * 2 + part renders part `part` of launch code order[slot] of frame f: its
-// 64 lanes carry the rays of wave tiles `part` (A) and `part + 2` (B) of the
-// 16x16 tile, vertically adjacent 8x8 tiles. Dynamic LDS: 2 x pair_rows x 64
-// floats (the two rays' budgets). Whole tiles only (no split codes), no
-// per-wave cost map (sr_wave_costs runs sr_integrate_kernel).
-__global__ __launch_bounds__(64, SR_PAIR_WAVES_PER_EU) void sr_integrate_pair_kernel(
-    const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
-    const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
-    size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
-    extern __shared__ float lds_pair[];
-    const unsigned B = (unsigned)fr.batch;
-    const unsigned bid = blockIdx.x;
-    const unsigned wg = bid >> 1;  // the tile's workgroup index (slot * B + f)
-    const int frame = B > 1 ? (int)(wg % B) : 0;
-    const unsigned slot = B > 1 ? wg / B : wg;
-    const int code = order ? order[slot] : ((int)slot << 8);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *count = 0;  // the shade kernel's queue (stream-ordered)
-    if (code < 0 || (code & SR_SPLIT)) return;
-    const int block = code >> 8;
-    if (order && wg < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
-    const int part = (int)(bid & 1u);
-    const int tA = part * 64 + (int)threadIdx.x, tB = tA + 128;
-    const size_t base = ((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256;
-    const PS ps{ps_base, ps_n};
-    Tex tx;
-    tx.bg = nullptr;
-    tx.arr = arr;
-    tx.opq = opq;
-    const int nb = sc->num_budget, ncyl = __builtin_popcount((unsigned)sc->budget_cyl_mask);
-    const int rows = SR_PAIR_ROWS(nb, ncyl);
-    float* const E0 = lds_pair + threadIdx.x;
-    PairRay A, Bq;
-    // camera ray (frag:859-889) of one ray; rays that end at once (flat, noise
-    // mask) write their record; off-frame threads do nothing
-    auto init = [&](PairRay& L, int t, float* E) {
-        L.n = 0;
-        L.force = false;
-        L.im = -1;
-        L.up = 0.0f;
-        L.T = 0.0f;
-        L.m = L.mh = INFINITY;
-        L.cm = 0u;
-        L.st = ST_DONE;
-        L.r.u = 2.0f / 3.0f;
-        L.r.du = 0.0f;
-        Pix q;
-        if (!pixel_of(fr, block, t, q)) return;  // parked, no record
-        const int st = init_pixel(fr, fr.cam[frame], q, L.r);
-        if (st >= 0) {
-            pair_finish(ps, base + t, L, st, 0, 0);
-            return;
-        }
-        L.st = -1;
-        Budget bs = pair_budget(L, E, nb + 1, nb + 1 + 2 * ncyl);
-        budget_init(sc, bs, L.r.ro, L.r.nv, L.r.tv, L.r.du < 0.0f && L.r.u < 0.6f, fr.out_dip);
-        pair_store_budget(L, bs);
-        L.rA = __builtin_amdgcn_rcpf(L.r.u);
-    };
-    init(A, tA, E0);
-    init(Bq, tB, E0 + (size_t)rows * SR_E_STRIDE);
-    int steps = 0;
-    if (A.st < 0 || Bq.st < 0) steps = integrate_pair(sc, segs, tbl, fr, tx, ps, base + tA, base + tB, E0, A, Bq);
-    if (cost) {  // all 64 lanes are active here
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
-        if ((threadIdx.x & 63) == 0) atomicMax(&cost[block], steps);
-    }
-}
-#endif
-
 // Launch order for the next frame: workgroup tiles by descending cost of this
 // frame (counting sort on 256 cost buckets), so the long rays - those
 // orbiting near the photon sphere run to max_steps - start first instead of
@@ -2778,13 +2387,6 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
-#if !defined(SR_PROF) && !defined(SR_STATS)
-    if (fr->pair && cull && !fr->wave_cost && !split) {
-        const size_t lds = 2u * (size_t)fr->pair_rows * SR_E_STRIDE * sizeof(float);
-        hipLaunchKernelGGL(sr_integrate_pair_kernel, dim3(slots * B * 2), dim3(64), lds, stream, sc, tbl, segs, arr,
-                           opq, *fr, ps, ps_n, count, order, cost);
-    } else
-#endif
     if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);

@@ -55,10 +55,6 @@ struct sr_ctx {
     uint8_t* d_opq = nullptr;  // texture-array opacity bitmap (make_opacity_map)
     bool scene_set = false;
     bool cull = true;
-#ifndef SR_PAIR_DEFAULT
-#define SR_PAIR_DEFAULT 1
-#endif
-    bool pair = SR_PAIR_DEFAULT != 0;  // two rays per lane where the frame allows it (build_frame)
     sr_dev_scene h_scene;
     // pixel pipeline scratch (geodesic.hip): SR_PS_FIELDS planes of ps_n floats,
     // the resume worklist and its counter; grown on demand, reused per frame.
@@ -634,15 +630,6 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.split_tiles = ctx->split_tiles;
     fr.split_log2 = ctx->split_log2;
     fr.split_min_steps = ctx->split_min_steps;
-    // two rays per lane: culled frames whose every object is budgeted and
-    // without the test-ray overlay (every chord exact otherwise), whole tiles
-    {
-        const sr_dev_scene& d = ctx->h_scene;
-        const int ncyl = __builtin_popcount((unsigned)d.budget_cyl_mask);
-        const int rows = 1 + d.num_budget + 3 * ncyl;
-        fr.pair_rows = rows > SR_MAX_BUDGET + 1 ? rows : SR_MAX_BUDGET + 1;
-        fr.pair = ctx->pair && ctx->cull && d.num_step == 0 && !d.tr_visible && ctx->split_tiles == 0 ? 1 : 0;
-    }
     return SR_OK;
 }
 
@@ -1079,14 +1066,6 @@ int sr_debug_last_order(sr_ctx* c, int* out, int max_n, int* n) {
 int sr_debug_set_culling(sr_ctx* c, int enabled) {
     if (!c) return SR_E_INVALID;
     c->cull = enabled != 0;
-    return SR_OK;
-}
-
-// Not in sr.h's public set: two rays per lane on or off (parity tests
-// compare both kernels bit for bit; A/B timing).
-int sr_debug_set_pair(sr_ctx* c, int enabled) {
-    if (!c) return SR_E_INVALID;
-    c->pair = enabled != 0;
     return SR_OK;
 }
 

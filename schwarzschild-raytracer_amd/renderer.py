@@ -48,10 +48,6 @@ class Renderer:
     def set_culling(self, enabled: bool) -> None:
         abi.check(self.lib.sr_debug_set_culling(self.ctx, 1 if enabled else 0), "sr_debug_set_culling")
 
-    def set_pair(self, enabled: bool) -> None:
-        """Two rays per lane (sr_integrate_pair_kernel) where the frame allows it; off: one ray per lane."""
-        abi.check(self.lib.sr_debug_set_pair(self.ctx, 1 if enabled else 0), "sr_debug_set_pair")
-
     def set_split(self, max_tiles: int, lanes_per_wave: int = 16, min_steps: int = 1) -> None:
         """Run the costliest tiles of the previous frame as sparse waves (sr_set_split; 0 tiles: off)."""
         abi.check(self.lib.sr_set_split(self.ctx, int(max_tiles), int(lanes_per_wave), int(min_steps)), "sr_set_split")

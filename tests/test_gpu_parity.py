@@ -605,43 +605,3 @@ def test_two_contexts_alternating_shapes_in_flight(pkg, textures):
                     assert np.array_equal(o[0, s_ * 8:s_ * 8 + n], full[b * 8:b * 8 + n]), (key, b)
     for c in ctxs:
         c.close()
-
-
-@pytest.mark.parametrize("seed", range(6))
-def test_two_rays_per_lane_bit_identical(pkg, gpu, seed):
-    """sr_integrate_pair_kernel (two rays per lane, RK4 packed across the
-    rays, one budget set per ray) against the one-ray kernel: float
-    FragColor, RGBA8 and step counts identical - the default camera at the
-    headline's step count, random cameras (reseeds beyond r = 100), batched
-    flyby frames and a rank's block list."""
-    import torch
-
-    sc, abi = pkg.scenes, pkg.abi
-    gpu.set_scene(sc.scene_default(textured=bool(seed % 2 == 0)))
-    gpu.set_test_ray(abi.default_test_ray())
-    cam = abi.default_camera() if seed == 0 else sc.random_camera(500 + seed)
-    if seed == 5:
-        cam = sc.camera_look((0.0, 12.0, 119.4), (0.0, -12.0, -119.4), fov=12.0)  # reseeds
-    params = abi.default_params(max_steps=2000 if seed < 2 else 1200, percent_black=-1.0)
-    W, H = (480, 270) if seed < 2 else (320, 184)
-    outs = []
-    for pair in (False, True):
-        gpu.set_pair(pair)
-        f, b, s = gpu.render_debug(cam, params, W, H)
-        torch.cuda.synchronize()
-        outs.append((f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()))
-    for a, b_, what in zip(outs[0], outs[1], ("float", "rgba8", "steps")):
-        assert np.array_equal(a, b_), f"{what} differs with two rays per lane (seed {seed})"
-    if seed == 0:  # batched flyby frames and a block list, both kernels
-        cams = [abi.camera_flyby((f + 0.5) / 4, 30.0, 10.0) for f in range(4)]
-        got = []
-        for pair in (False, True):
-            gpu.set_pair(pair)
-            for _ in range(2):
-                o, rows = gpu.render_blocks_batch(cams, params, W, H, 8, 0, 1)
-            l = gpu.render_block_list(cams, params, W, H, 8, [3, 0, 17, -1, 9])
-            torch.cuda.synchronize()
-            l = l.cpu().numpy()
-            got.append((o.cpu().numpy()[:, :rows], np.concatenate([l[:, :24], l[:, 32:]], axis=1)))  # slot 3: -1
-        assert np.array_equal(got[0][0], got[1][0]) and np.array_equal(got[0][1], got[1][1])
-    gpu.set_pair(True)

@@ -12,7 +12,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
-NAMES = {0: "wave_steps", 1: "events", 11: "unused", 12: "object_tests", 13: "lane_steps"}
+NAMES = {0: "wave_steps", 1: "events", 11: "coast_wave_steps", 12: "object_tests", 13: "lane_steps"}
 
 
 def main():
