@@ -139,6 +139,10 @@ def parse():
                     help="N > 1: cost: each rank renders an equal number of 8-row blocks of about equal cost "
                          "(dist.balanced_blocks over the frame's step map, sr_render_block_list); cyclic: block b "
                          "on rank b %% N")
+    ap.add_argument("--reprice", type=int, default=-1,
+                    help="N > 1, --balance cost: re-price the block lists every this many launches from a "
+                         "quarter-resolution cost map of the launch's camera (rank 0, broadcast); -1: every "
+                         "launches-in-flight launches with --camera flyby, else never; 0: never")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl: RCCL gather of device tiles over xGMI (one GPU per rank); gloo: tiles staged "
                          "through host memory (ranks may share a GPU)")
@@ -257,11 +261,14 @@ def main():
                     frames[first + i] = batch[i].clone()  # on the launch's stream (nccl) or host (gloo)
 
     lists = [None]  # balanced_blocks lists (N > 1, --balance cost), set below from the step map
+    ctx_lists = [None] * F  # the lists each context's current launch renders (re-pricing changes them)
+    rp = {"every": 0, "count": 0, "pricer": None, "stream": None, "lists": None}  # flyby re-pricing (set below)
 
-    def render(rk, first, n, out, s_k):
+    def render(rk, first, n, out, s_k, lst=None):
         """frames first .. first + n - 1 of this rank's share into out[:n]"""
-        if lists[0] is not None:
-            rk.render_block_list(cams[first:first + n], params, W, H, BLOCK_ROWS, lists[0][rank], out=out[:n],
+        lst = lst if lst is not None else lists[0]
+        if lst is not None:
+            rk.render_block_list(cams[first:first + n], params, W, H, BLOCK_ROWS, lst[rank], out=out[:n],
                                  stream=s_k)
         elif n == 1:
             rk.render_blocks(cams[first], params, W, H, BLOCK_ROWS, rank, world, out=out[0], stream=s_k)
@@ -271,10 +278,34 @@ def main():
 
     gtime = {"on": False, "events": [], "host_s": 0.0}  # the timed launches' gathers (N > 1)
 
+    def reprice(cam):
+        """Lists for a moved camera (collective): rank 0 prices the blocks
+        from a quarter-resolution cost map of `cam` on its own context and
+        stream (the launches in flight run on), every rank gets its lists."""
+        obj = [None]
+        if rank == 0:
+            wl, hl = max(8, W // 4), max(8, H // 4)
+            wc = rp["pricer"].wave_costs(cam, params, wl, hl, stream=rp["stream"])
+            rp["stream"].synchronize()
+            # a quarter-resolution 8-row block spans four full-resolution ones
+            cl = D.block_costs(wc.cpu())
+            obj = [D.balanced_blocks(np.repeat(cl, 4)[:D.nblocks(H, BLOCK_ROWS)], world)]
+        dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
+        rp["count"] += 1
+        return obj[0]
+
     def launch(j, first, n):
         rk, tile_k, gather_k, s_k, host_k = ctxs[j % F]
         with torch.cuda.stream(s_k):
-            render(rk, first, n, tile_k, s_k)
+            if rp["every"] and first > 0 and (first // B) % rp["every"] == 0:
+                rp["lists"] = reprice(cams[first])
+            if ctx_lists[j % F] is not rp["lists"]:
+                # every context takes the newest lists at its next launch: its
+                # previous launch was gathered (launch order), so this launch's
+                # render and gather use them together
+                ctx_lists[j % F] = rp["lists"]
+                gather_k.set_lists(rp["lists"])
+            render(rk, first, n, tile_k, s_k, ctx_lists[j % F])
             if gloo:
                 host_k[:n].copy_(tile_k[:n], non_blocking=True)
                 return
@@ -331,9 +362,19 @@ def main():
                           "lists_from": "rank 0 (broadcast)"})]
         dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
         lists[0], balance = obj[0]
-        for c in ctxs:
+        for k, c in enumerate(ctxs):
             c[2].set_lists(lists[0])
+            ctx_lists[k] = lists[0]
+        rp["lists"] = lists[0]
         rows_mine = D.rows_of_list(lists[0][rank], H, BLOCK_ROWS)
+        # a moving camera: re-price every `every` launches
+        rp["every"] = args.reprice if args.reprice >= 0 else (F if args.camera == "flyby" else 0)
+        if rp["every"] and rank == 0:
+            rp["pricer"] = pkg.Renderer(dev.index)
+            rp["pricer"].set_scene(scene)
+            rp["pricer"].set_background(skybox)
+            rp["pricer"].set_texture_array(arr)
+            rp["stream"] = torch.cuda.Stream(dev)
     else:
         rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
     sigma_steps_frame = int(steps_full.sum().item())
@@ -412,6 +453,20 @@ def main():
         speedup_ref = {"culled_ms": round(culled, 4), "reference_loop_ms": round(unculled, 4),
                        "speedup": round(unculled / culled, 2)}
 
+    if balance is not None and rp["every"]:
+        balance["reprice_every_launches"] = rp["every"]
+        balance["repriced"] = rp["count"]
+        if rank == 0:  # how even the frame-0 lists and the lists in use are on the last timed camera
+            last_cam = cams[warm + args.steps - 1]
+            cost_last = D.block_costs(r.wave_costs(last_cam, params, W, H, stream=stream).cpu())
+
+            def mom(lst):
+                loads = [sum(cost_last[b] for b in l if b >= 0) for l in lst]
+                return round(max(loads) / (sum(loads) / world), 4)
+
+            balance["last_camera_max_over_mean"] = {"frame0_lists": mom(lists[0]),
+                                                    "lists_in_use": mom(ctx_lists[(len(range(warm, warm + args.steps, B)) - 1) % F]),
+                                                    "cyclic": mom([D.blocks_of(k, world, H, BLOCK_ROWS) for k in range(world)])}
     ranks = None
     if distributed:  # max over ranks (RCCL reduces device tensors, gloo host ones)
         t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=None if gloo else dev)
@@ -527,6 +582,8 @@ def main():
         dist.destroy_process_group()
     for c in ctxs:
         c[0].close()
+    if rp["pricer"] is not None:
+        rp["pricer"].close()
 
 
 FRAME_HASHES = ROOT / "tests" / "golden" / "frame_hashes.npz"

@@ -20,7 +20,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
-ARGS = ["--width", "320", "--height", "180", "--max-steps", "800", "--steps", "6", "--warmup", "2",
+ARGS = ["--width", "320", "--height", "180", "--max-steps", "800", "--steps", "12", "--warmup", "2",
         "--inflight", "3", "--camera", "flyby", "--cpu-baseline", "off", "--critical-path", "off",
         "--reference-loop", "off"]
 
@@ -58,9 +58,16 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
     else:
         assert bal is None
     assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["launches_in_flight"] == 3
+    ranks = multi["config"]["ranks"]  # the N-rank line documents every rank
+    assert [r["rank"] for r in ranks] == list(range(world)) and all(r["world_size"] == world for r in ranks)
+    assert all(r["share_ms_per_frame"] > 0 and r["gather_ms_per_frame"] >= 0 for r in ranks)
+    if balance == "cost":  # the flyby re-prices the lists while frames are in flight
+        assert bal["lists_from"] == "rank 0 (broadcast)" and bal["repriced"] >= 1, bal
+        lc = bal["last_camera_max_over_mean"]
+        assert lc["lists_in_use"] >= 1.0 and lc["frame0_lists"] >= 1.0
     one = sorted((tmp_path / "one").glob("frame_*.npy"))
     many = sorted((tmp_path / "multi").glob("frame_*.npy"))
-    assert len(one) == len(many) == 6
+    assert len(one) == len(many) == 12
     distinct = set()
     for a, b in zip(one, many):
         assert a.name == b.name
@@ -68,4 +75,4 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
         assert fa.shape == fb.shape == (180, 320, 4)
         assert np.array_equal(fa, fb), a.name
         distinct.add(fa.tobytes())
-    assert len(distinct) == 6  # the flyby moves the camera every frame
+    assert len(distinct) == 12  # the flyby moves the camera every frame

@@ -217,3 +217,32 @@ def test_cpp_multi_gpu_driver_frame(pkg, fh, assets, tmp_path):
     assert line["world_size"] == 1 and line["frames"] == 4 and line["ranks"][0]["render_ms_per_frame"] > 0
     frame = np.frombuffer(out.read_bytes(), dtype=np.uint8).reshape(H, W, 4)
     compare(pkg, fh, "c3", frame, None, "C++ RCCL driver")
+
+
+def test_frame_gather_device_reassembly(pkg, fh, assets):
+    """bench.py's FrameGather on device tiles (the nccl path without the
+    collective: world 1): a cost-balanced list rendered by
+    sr_render_block_list, reassembled by sr_assemble_blocks into the
+    gather's frame buffer, equals the oracle's headline frame; then three
+    frames of a batch."""
+    import torch
+
+    W, H, N = (int(v) for v in fh["c3/config"])
+    abi, D = pkg.abi, pkg.dist
+    r = renderer(pkg, assets, "2k")
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    cam = abi.default_camera()
+    costs = D.block_costs(r.wave_costs(cam, params, W, H))
+    lists = D.balanced_blocks(costs[::-1].copy(), 1)  # one rank: every block, in some order
+    lists = [sorted(lists[0], key=lambda b: (b * 7) % 135)]  # a permuted list exercises the reassembly
+    tile = torch.zeros((3, len(lists[0]) * BLOCK_ROWS, W, 4), dtype=torch.uint8, device="cuda")
+    g = D.FrameGather(tile, 1, 0, H, BLOCK_ROWS)
+    g.set_lists(lists)
+    for _ in range(2):
+        r.render_block_list([cam] * 3, params, W, H, BLOCK_ROWS, lists[0], out=tile)
+        frames = g(3)
+    torch.cuda.synchronize()
+    assert tuple(frames.shape) == (3, H, W, 4)
+    for f in range(3):
+        compare(pkg, fh, "c3", frames[f].cpu().numpy(), None, f"FrameGather frame {f}")
+    r.close()

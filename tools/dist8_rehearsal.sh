@@ -13,4 +13,12 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 
   --master-port 29517 bench.py --gpus 8 --steps 20 --warmup 3 --dist-backend gloo > "$OUT/bench8.log" 2>&1 \
   || { echo "bench8 rc=$?"; tail -n 30 "$OUT/bench8.log"; exit 1; }
 grep '^{' "$OUT/bench8.log" > "$OUT/bench8.json"; cat "$OUT/bench8.json"
+# the flyby at N = 8: lists re-priced every 3 launches (default) and frame-0 lists kept
+for rp in -1 0; do
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+    --master-port 29518 bench.py --gpus 8 --steps 40 --warmup 3 --dist-backend gloo --camera flyby --reprice $rp \
+    --cpu-baseline off > "$OUT/bench8_flyby_rp$rp.log" 2>&1 || { echo "bench8 flyby rc=$?"; tail -n 30 "$OUT/bench8_flyby_rp$rp.log"; exit 1; }
+  grep '^{' "$OUT/bench8_flyby_rp$rp.log" > "$OUT/bench8_flyby_rp$rp.json"
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], json.dumps(d['config']['balance']))" "$OUT/bench8_flyby_rp$rp.json"
+done
 echo "session done"
