@@ -1560,32 +1560,35 @@ __device__ __forceinline__ float point_err(float rA, float rB) { return 4.0e-6f 
 __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 
 // rk4_step, frag:341-355, plus the `u += .x; du += .y` of frag:918-919 (h6 =
-// `delta_phi / 6.` and hh = 0.5 h, computed on the host). The u and u' halves
-// of each stage are the same operations on different operands, so they run
-// as packed binary32 pairs (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32: two
-// correctly rounded results per lane):
+// `delta_phi / 6.` and hh = 0.5 h, computed on the host):
 //   (ua, k2) = (u, u') + (k1, l1) hh           l2 = ddu(ua)
 //   (ub, k3) = (u, u') + (k2, l2) hh           l3 = ddu(ub)
 //   (uc, k4) = (u, u') + (k3, l3) h            l4 = ddu(uc)
 //   (u, u') += h6 ((fma(2, (k3, l3), fma(2, (k2, l2), (k1, l1)))) + (k4, l4))
-// Bit-identical to the reference's expressions: (0.5 q) h and q (0.5 h) are
+// in scalar binary32 instructions. The u and u' halves of a stage are the
+// same operations on different operands; as packed pairs (v_pk_mul_f32 /
+// v_pk_add_f32 / v_pk_fma_f32, SR_PACKED_RK4) they are half the instructions
+// but each takes the SIMD's issue for twice as long as a scalar one, and
+// need hazard s_nops: with six waves per SIMD the scalar form renders 2.9 %
+// more frames per second (one frame alone, latency bound, is 3.5 % slower;
+// profiles/r03/s13_*). Bit-identical to the reference's expressions: (0.5 q) h and q (0.5 h) are
 // both the rounding of the same product, as scaling by 0.5 is exact for
 // non-subnormal q (the stage values here are never subnormal: DESIGN.md §4);
 // and 2 q is exact, so fma(2, q, a) is the rounding of a + 2 q, as the
 // reference's a + (2. * q).
 typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, float h6, float& un, float& dun) {
-#ifdef SR_SCALAR_RK4
+#ifndef SR_PACKED_RK4
     const float k1 = du;
     const float l1 = ddu(u);
-    const float k2 = du + 0.5f * l1 * h;
-    const float l2 = ddu(u + 0.5f * k1 * h);
-    const float k3 = du + 0.5f * l2 * h;
-    const float l3 = ddu(u + 0.5f * k2 * h);
+    const float k2 = du + l1 * hh;
+    const float l2 = ddu(u + k1 * hh);
+    const float k3 = du + l2 * hh;
+    const float l3 = ddu(u + k2 * hh);
     const float k4 = du + l3 * h;
     const float l4 = ddu(u + k3 * h);
-    un = u + h6 * (k1 + 2.0f * k2 + 2.0f * k3 + k4);
-    dun = du + h6 * (l1 + 2.0f * l2 + 2.0f * l3 + l4);
+    un = u + h6 * (__builtin_fmaf(2.0f, k3, __builtin_fmaf(2.0f, k2, k1)) + k4);
+    dun = du + h6 * (__builtin_fmaf(2.0f, l3, __builtin_fmaf(2.0f, l2, l1)) + l4);
 #else
     // Each stage's (u_stage, k) pair is overwritten in place by (l, k) =
     // (ddu(u_stage), k); the next stage reads it swapped (op_sel), so no
