@@ -1406,9 +1406,11 @@ __device__ __forceinline__ uint32_t unorm8(float x) {
 // hand-off 2.4x its size):
 //   every pixel      one 16-byte store {packed word, rd} (rd: the final
 //                    direction, read by escaped and flat rays)
-//   logged hits      one 32-byte record each {p, key | steps << 8, dir}; a
-//                    ray that ends in the black hole gets status ST_BH
-//                    instead (its colour is a constant, shade_hit)
+//   logged hits      one 32-byte record each {p, key | steps << 8, dir},
+//                    hit-major (hit j of neighbouring pixels adjacent: a
+//                    wave's records share lines, 150 -> 126 MB per headline
+//                    frame); a ray that ends in the black hole gets status
+//                    ST_BH instead (its colour is a constant, shade_hit)
 //   ST_FLAT          ro (plane)
 //   ST_MORE          the resumable state (planes): the log filled with
 //                    translucent hits; sr_resume_kernel continues the ray
@@ -1416,7 +1418,7 @@ __device__ __forceinline__ uint32_t unorm8(float x) {
 // shade kernel always finishes it: it keeps no resumable state.
 enum {
     PS_REC = 0,                       // [4 floats / px] word, rd[3]
-    PS_HITS = 4,                      // [8 floats / hit] p[3], (key + 24) | steps << 8, dir[3], -
+    PS_HITS = 4,                      // [8 floats / hit, (j * n + id) * 8] p[3], (key + 24) | steps << 8, dir[3], -
     PS_PLANES = 4 + 8 * SR_PS_HITS,   // planes (field * n + id) from here:
     PS_I = 0, PS_FRAG = 1, PS_RO = 5, PS_NV = 8, PS_TV = 11, PS_U = 14, PS_DU = 15
 };
@@ -1470,7 +1472,7 @@ struct PS {
     }
     __device__ __forceinline__ float4 get_rec(size_t id) const { return *reinterpret_cast<const float4*>(p + 4 * id); }
     __device__ __forceinline__ float* hit(size_t id, int j) const {
-        return p + 4 * n + (id * SR_PS_HITS + (size_t)j) * 8;
+        return p + 4 * n + ((size_t)j * n + id) * 8;
     }
     // planes of the resumable / flat-ray state
     __device__ __forceinline__ float& at(int f, size_t id) const { return p[(size_t)(PS_PLANES + f) * n + id]; }
@@ -1977,14 +1979,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (!RECORD) return ST_HIT;
                 if (hit.slot == SLOT_BH) return ST_BH;  // opaque black (shade_hit): no record
                 // r.steps: the ray's step count if this hit ends it
-                float* h = log.ps.hit(log.id, log.n);
-                h[0] = hit.p.x;
-                h[1] = hit.p.y;
-                h[2] = hit.p.z;
-                h[3] = __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (r.steps << 8));
-                h[4] = r.rd.x;
-                h[5] = r.rd.y;
-                h[6] = r.rd.z;
+                // the whole 32-byte sector in two 16-byte stores (a partial
+                // sector costs a read-modify-write)
+                float4* h = reinterpret_cast<float4*>(log.ps.hit(log.id, log.n));
+                h[0] = make_float4(hit.p.x, hit.p.y, hit.p.z,
+                                   __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (r.steps << 8)));
+                h[1] = make_float4(r.rd.x, r.rd.y, r.rd.z, 0.0f);
                 log.n++;
                 if (op == OP_OPAQUE) return ST_HIT;
                 if (log.n == SR_PS_HITS) return ST_MORE;
