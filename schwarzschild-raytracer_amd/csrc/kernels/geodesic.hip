@@ -551,9 +551,30 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
 #define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
+// The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
+// joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
+// the step's angle dphi at the origin, so it stays in the half-plane beyond
+// the chord between the same directions at the smaller radius: at least
+// min(rA, rB) cos(dphi / 2) from the origin. While u <= SR_BH_U (r >=
+// 1.0142) at both ends, a chord keeps 0.0076 clear of the black hole's reach
+// region (the r = 1 shell grown by mu S, slot_reachable: r <= 1.0066 for S <=
+// 2.8 there), so a lane outside that radius needs no distance budget for the
+// hole at all: its slot-0 budget is +inf and the step loop exits on u >
+// uhi = SR_BH_U instead (one compare per step), where slot 0 re-anchors and
+// the chord is reach-tested. Lanes inside the band (or the shell) keep the
+// distance budget, uhi = +inf. Ring rays orbit the photon sphere at r ~ 1.5
+// for hundreds of steps: their distance budgets (0.5 at r = 1.5) ran out
+// every ~50 steps per lane and made the hole the most frequent event.
+#ifndef SR_BH_WINDOW
+#define SR_BH_WINDOW 1
+#endif
+#define SR_BH_U 0.986f      // u at r = 1.01420
+#define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
+
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
+    float uhi;  // the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none)
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
     float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
                   // covers chords nearly parallel to an axis
@@ -607,6 +628,11 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
     {
         float e = clearance_bh(a);
+        bs.uhi = INFINITY;
+        if (SR_BH_WINDOW && a > SR_BH_RWIN) {
+            e = INFINITY;
+            bs.uhi = SR_BH_U;
+        }
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
         bs.E[0] = e;
         m = nmin(m, e);
@@ -767,7 +793,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
-                                                 bool outward, float dip) {
+                                                 bool outward, float dip, bool bhx) {
     constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -786,7 +812,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             }
         }
     }
-    uint32_t forced = 0;  // this lane's slots whose E does not cover the chord
+    // this lane's slots whose E does not cover the chord (bit 0: the chord
+    // left the black hole's u window, bhx)
+    uint32_t forced = (uint32_t)bhx;
     {
         uint32_t c = cyl;
 #pragma unroll
@@ -863,7 +891,10 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         // (the others re-anchor early: look-ahead, or another lane spent it)
         const bool h = (hard >> j) & 1u;
         if (j == 0) {
-            const float v = (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip))
+            // beyond the band: the u window instead of a distance budget
+            const bool win = SR_BH_WINDOW && a - perr > SR_BH_RWIN;
+            bs.uhi = win ? SR_BH_U : INFINITY;
+            const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
             bs.E[0] = v;
@@ -1642,6 +1673,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     bs.E = lds_E + threadIdx.x;
     bs.pa0 = SR_E_PA0;
     bs.slab0 = SR_E_SLAB0;
+    bs.uhi = INFINITY;
     if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
@@ -1773,8 +1805,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
-                // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord)
-                return __ballot(!(Tn < lim) || un < fr.u_f);
+                // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord);
+                // un > uhi: the chord left the black hole's u window
+                return __ballot(!(Tn < lim) || un < fr.u_f || un > bs.uhi);
             };
             // apply step i and move to entry (en, en1) of step i + 1
             auto apply = [&](float4 en, float4 en1) -> bool {
@@ -1838,7 +1871,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(0, 1);
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
-                    if (__ballot(un < fr.u_f)) {
+                    if (__ballot(un < fr.u_f || un > bs.uhi)) {
 #pragma unroll
                         for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
@@ -1876,7 +1909,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             settle_prev(i);
             return ST_BG;
         }
-        const bool event = !(Tn < lim);
+        const bool bhx = un > bs.uhi;  // the chord left the black hole's u window
+        const bool event = !(Tn < lim) || bhx;
         // slots about to run out re-anchor at this event too (within SR_AHEAD
         // of this chord's length plus SR_AHEAD_T of the path since the last
         // event): fewer events, each re-anchoring more
@@ -1948,7 +1982,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
-                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
+                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                                     bhx);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
