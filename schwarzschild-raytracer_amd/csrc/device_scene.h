@@ -184,6 +184,9 @@ typedef struct {
     int32_t split_tiles;
     int32_t split_log2;
     int32_t split_min_steps;
+    // 1: every chord origin lies within r = 100 (u_f >= 0.01 and the cameras
+    // inside), where the black hole's u window holds (geodesic.hip SR_BH_WINDOW)
+    int32_t win_ok;
 } sr_dev_frame;
 
 #endif

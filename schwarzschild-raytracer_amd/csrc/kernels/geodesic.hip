@@ -555,21 +555,33 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
 // the step's angle dphi at the origin, so it stays in the half-plane beyond
 // the chord between the same directions at the smaller radius: at least
-// min(rA, rB) cos(dphi / 2) from the origin. While u <= SR_BH_U (r >=
-// 1.0142) at both ends, a chord keeps 0.0076 clear of the black hole's reach
-// region (the r = 1 shell grown by mu S, slot_reachable: r <= 1.0066 for S <=
-// 2.8 there), so a lane outside that radius needs no distance budget for the
-// hole at all: its slot-0 budget is +inf and the step loop exits on u >
-// uhi = SR_BH_U instead (one compare per step), where slot 0 re-anchors and
-// the chord is reach-tested. Lanes inside the band (or the shell) keep the
-// distance budget, uhi = +inf. Ring rays orbit the photon sphere at r ~ 1.5
-// for hundreds of steps: their distance budgets (0.5 at r = 1.5) ran out
-// every ~50 steps per lane and made the hole the most frequent event.
+// min(rA, rB) cos(dphi / 2) >= min(rA, rB) out_dip from the origin. While u
+// <= SR_BH_U (r >= 1.0142) at both ends and out_dip > SR_BH_DIP, every point
+// of a chord is at least r_e = 1.0076 from the origin, and sphere_test
+// cannot accept it: a root on the r = 1 sphere needs a computed discriminant
+// b^2 - c >= 0 (true value 1 - rho^2 for the line at distance rho) and a root
+// inside [0, len], i.e. within the segment, whose end is sqrt(r_e^2 - rho^2)
+// - sqrt(1 - rho^2) >= (r_e^2 - 1) / (2 r_e) = 0.0076 along the line from
+// the true root (the line's foot point beyond it when rho >= r_e). With the
+// chord origin o within r = 100 (sr_dev_frame.win_ok: u_f >= 0.01, cameras
+// inside) the discriminant is computed within 4 eps |o|^2 = 4.8e-3 and the
+// root within that over 2 sqrt(disc) (or its square root, 0.07, near
+// tangency, where the distance is 0.12 or more): at most 0.0024 at rho = 0
+// and 3x below the distance everywhere. So a lane beyond that radius needs
+// no distance budget for the hole: its slot-0 budget is +inf and the step
+// loop exits on u > uhi = SR_BH_U instead (one compare per step), where slot
+// 0 re-anchors and the chord is reach-tested. Lanes inside the band (or the
+// shell) keep the distance budget, uhi = +inf. Ring rays orbit the photon
+// sphere at r ~ 1.5 for hundreds of steps: their distance budgets (0.5 at r =
+// 1.5) ran out every ~50 steps per lane and made the hole the most frequent
+// event (profiles/r03/s19_*: its re-anchors 186 k -> 93 k per headline frame,
+// a frame alone -8 %).
 #ifndef SR_BH_WINDOW
 #define SR_BH_WINDOW 1
 #endif
 #define SR_BH_U 0.986f      // u at r = 1.01420
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
+#define SR_BH_DIP 0.9935f   // 1.0142 x 0.9935 = 1.0076
 
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
@@ -620,7 +632,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 }
 
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv,
-                                            bool outward, float dip) {
+                                            bool outward, float dip, bool bh_ok) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
@@ -629,7 +641,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     {
         float e = clearance_bh(a);
         bs.uhi = INFINITY;
-        if (SR_BH_WINDOW && a > SR_BH_RWIN) {
+        if (SR_BH_WINDOW && bh_ok && a > SR_BH_RWIN) {
             e = INFINITY;
             bs.uhi = SR_BH_U;
         }
@@ -793,7 +805,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
-                                                 bool outward, float dip, bool bhx) {
+                                                 bool outward, float dip, bool bhx, bool bh_ok) {
     constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -892,7 +904,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         const bool h = (hard >> j) & 1u;
         if (j == 0) {
             // beyond the band: the u window instead of a distance budget
-            const bool win = SR_BH_WINDOW && a - perr > SR_BH_RWIN;
+            const bool win = SR_BH_WINDOW && bh_ok && a - perr > SR_BH_RWIN;
             bs.uhi = win ? SR_BH_U : INFINITY;
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
@@ -1674,7 +1686,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     bs.pa0 = SR_E_PA0;
     bs.slab0 = SR_E_SLAB0;
     bs.uhi = INFINITY;
-    if (CULL) budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip);
+    if (CULL)
+        budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                    fr.win_ok && fr.out_dip > SR_BH_DIP);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -1983,7 +1997,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                     bhx);
+                                     bhx, fr.win_ok && fr.out_dip > SR_BH_DIP);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);

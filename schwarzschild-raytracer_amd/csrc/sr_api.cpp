@@ -648,6 +648,12 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     if (rc != SR_OK) return rc;
     for (int f = 1; f < n_frames; f++) build_cam(&cams[f], fr.cam[f]);
     fr.batch = n_frames;
+    // the black hole's u window (geodesic.hip SR_BH_WINDOW): chord origins within r = 100
+    fr.win_ok = fr.uf_radius <= 100.5f;
+    for (int f = 0; f < n_frames; f++) {
+        const float* q = fr.cam[f].pos;
+        if (!((double)q[0] * q[0] + (double)q[1] * q[1] + (double)q[2] * q[2] <= 1.0e4)) fr.win_ok = 0;
+    }
     if (nrows < 0 || block_rows <= 0) return SR_E_INVALID;
     if (out && pitch < (size_t)width * 4) return SR_E_INVALID;
     if (n_frames > 1 && (!out || frame_stride < pitch * (size_t)nrows || dbg_rgba || dbg_steps)) return SR_E_INVALID;
