@@ -261,8 +261,8 @@ def main():
                     frames[first + i] = batch[i].clone()  # on the launch's stream (nccl) or host (gloo)
 
     lists = [None]  # balanced_blocks lists (N > 1, --balance cost), set below from the step map
-    ctx_lists = [None] * F  # the lists each context's current launch renders (re-pricing changes them)
-    rp = {"every": 0, "count": 0, "pricer": None, "stream": None, "lists": None}  # flyby re-pricing (set below)
+    sched = [None]  # dist.ListSchedule: the lists each context's launches render (re-pricing changes them)
+    rp = {"every": 0, "pricer": None, "stream": None}  # flyby re-pricing (set below)
 
     def render(rk, first, n, out, s_k, lst=None):
         """frames first .. first + n - 1 of this rank's share into out[:n]"""
@@ -291,21 +291,17 @@ def main():
             cl = D.block_costs(wc.cpu())
             obj = [D.balanced_blocks(np.repeat(cl, 4)[:D.nblocks(H, BLOCK_ROWS)], world)]
         dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
-        rp["count"] += 1
         return obj[0]
 
     def launch(j, first, n):
         rk, tile_k, gather_k, s_k, host_k = ctxs[j % F]
         with torch.cuda.stream(s_k):
-            if rp["every"] and first > 0 and (first // B) % rp["every"] == 0:
-                rp["lists"] = reprice(cams[first])
-            if ctx_lists[j % F] is not rp["lists"]:
-                # every context takes the newest lists at its next launch: its
-                # previous launch was gathered (launch order), so this launch's
-                # render and gather use them together
-                ctx_lists[j % F] = rp["lists"]
-                gather_k.set_lists(rp["lists"])
-            render(rk, first, n, tile_k, s_k, ctx_lists[j % F])
+            lst = None
+            if sched[0] is not None:
+                lst, changed = sched[0].adopt(j, reprice(cams[first]) if sched[0].due(first) else None)
+                if changed:
+                    gather_k.set_lists(lst)
+            render(rk, first, n, tile_k, s_k, lst)
             if gloo:
                 host_k[:n].copy_(tile_k[:n], non_blocking=True)
                 return
@@ -362,13 +358,12 @@ def main():
                           "lists_from": "rank 0 (broadcast)"})]
         dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
         lists[0], balance = obj[0]
-        for k, c in enumerate(ctxs):
+        for c in ctxs:
             c[2].set_lists(lists[0])
-            ctx_lists[k] = lists[0]
-        rp["lists"] = lists[0]
         rows_mine = D.rows_of_list(lists[0][rank], H, BLOCK_ROWS)
         # a moving camera: re-price every `every` launches
         rp["every"] = args.reprice if args.reprice >= 0 else (F if args.camera == "flyby" else 0)
+        sched[0] = D.ListSchedule(lists[0], F, rp["every"], B)
         if rp["every"] and rank == 0:
             rp["pricer"] = pkg.Renderer(dev.index)
             rp["pricer"].set_scene(scene)
@@ -455,7 +450,7 @@ def main():
 
     if balance is not None and rp["every"]:
         balance["reprice_every_launches"] = rp["every"]
-        balance["repriced"] = rp["count"]
+        balance["repriced"] = sched[0].count
         if rank == 0:  # how even the frame-0 lists and the lists in use are on the last timed camera
             last_cam = cams[warm + args.steps - 1]
             cost_last = D.block_costs(r.wave_costs(last_cam, params, W, H, stream=stream).cpu())
@@ -465,7 +460,7 @@ def main():
                 return round(max(loads) / (sum(loads) / world), 4)
 
             balance["last_camera_max_over_mean"] = {"frame0_lists": mom(lists[0]),
-                                                    "lists_in_use": mom(ctx_lists[(len(range(warm, warm + args.steps, B)) - 1) % F]),
+                                                    "lists_in_use": mom(sched[0].ctx[(len(range(warm, warm + args.steps, B)) - 1) % F]),
                                                     "cyclic": mom([D.blocks_of(k, world, H, BLOCK_ROWS) for k in range(world)])}
     ranks = None
     if distributed:  # max over ranks (RCCL reduces device tensors, gloo host ones)

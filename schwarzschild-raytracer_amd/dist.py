@@ -262,6 +262,36 @@ def assemble(stacked, world: int, height: int, block_rows: int):
     return v.reshape((per * world * block_rows,) + rest)[:height]
 
 
+class ListSchedule:
+    """The rank lists each launch renders when a moving camera re-prices them
+    (bench.py --reprice). Launch j runs on context j % contexts; a launch whose
+    first frame starts a new group of `every` launches (first // B % every ==
+    0) gets new lists (priced by the caller for its first camera), and every
+    context adopts the newest lists at its next launch: its previous launch was
+    gathered in launch order, so that launch's render and gather switch
+    together."""
+
+    def __init__(self, lists, contexts: int, every: int, frames_per_launch: int):
+        self.current = lists
+        self.ctx = [lists] * contexts
+        self.every = every
+        self.B = frames_per_launch
+        self.count = 0  # re-pricings so far
+
+    def due(self, first: int) -> bool:
+        return bool(self.every) and first > 0 and (first // self.B) % self.every == 0
+
+    def adopt(self, j: int, new=None):
+        """(lists for launch j, whether its context switched to them)"""
+        if new is not None:
+            self.current = new
+            self.count += 1
+        k = j % len(self.ctx)
+        changed = self.ctx[k] is not self.current
+        self.ctx[k] = self.current
+        return self.current, changed
+
+
 class FrameGather:
     """Preallocated gather of equal-size tiles to rank 0 (collective). A tile
     of [B, tile_rows, W, C] holds B frames (a batched launch); __call__(n)

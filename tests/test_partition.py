@@ -84,3 +84,29 @@ def test_cpp_multi_gpu_driver_builds_and_runs_help():
         pytest.skip("examples/bin/sr_multi_gpu not built (make -C schwarzschild-raytracer_amd)")
     r = subprocess.run([str(exe), "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "--gpus" in r.stdout and "WORLD_SIZE" in r.stdout
+
+
+def test_list_schedule_every_context_adopts_repriced_lists(pkg):
+    """bench.py --reprice (dist.ListSchedule): after a re-pricing every context
+    renders the new lists from its next launch on, and a launch's render and
+    gather always use the same lists (its context switches only between its
+    own launches)."""
+    D = pkg.dist
+    for F, every, B in ((3, 3, 10), (3, 1, 8), (2, 2, 16), (4, 3, 1)):
+        sched = D.ListSchedule("L0", F, every, B)
+        versions = ["L0"]
+        seen = {}  # context -> lists of its last launch
+        for j, first in enumerate(range(B * F, B * F + 40 * B, B)):  # after warmup, launches of B frames
+            new = None
+            if sched.due(first):
+                new = f"L{len(versions)}"
+                versions.append(new)
+            lst, changed = sched.adopt(j, new)
+            k = j % F
+            assert lst == versions[-1]  # the newest lists, from this launch on
+            assert changed == (seen.get(k, "L0") != lst)
+            seen[k] = lst
+        assert sched.count == len(versions) - 1 and sched.count >= 40 // every - 1
+    never = D.ListSchedule("L0", 3, 0, 8)
+    assert not any(never.due(f) for f in range(0, 400, 8))
+    assert never.adopt(5) == ("L0", False)
