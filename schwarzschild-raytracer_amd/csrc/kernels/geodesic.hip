@@ -350,6 +350,17 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // budget instead (clearance_slab, chord_parallel). Computed with
 // hardware sqrt: its error is far below the margins.
 #define SR_PATH_SLACK 1.01f
+// Ball form of the budgets (SR_BALL): a budget bounds the
+// displacement from the last budget event's end point instead of the path
+// since it, so the step loop tests the step's end point against a ball
+// (sign of a quadratic in u, no reciprocal or square root) instead of
+// summing chord-length bounds. Every margin below that assumed chords within
+// a window of path W holds for chords within a ball of radius W, except the
+// chord length (up to 2 W) and the directional plane window (a path bound,
+// converted in plane_window).
+#ifndef SR_BALL
+#define SR_BALL 1
+#endif
 #ifndef SR_NEAR
 #define SR_NEAR 1.0f
 #endif
@@ -394,7 +405,8 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
             // the window's path is at most this clearance (capped): chord
             // origins stay within sqrt(3) W of A, chords within W long
             const float W = fminf(c, SR_BUDGET_TMAX);
-            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + (3.0f * W + 1.0f);
+            // (chords of a ball of radius W are up to 2 W long: SR_BALL)
+            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + ((SR_BALL ? 4.0f : 3.0f) * W + 1.0f);
             float qm = (Sb * Sb) * sl.qk;
             c = fminf(c - qm, SR_BUDGET_TMAX);
         }
@@ -439,7 +451,16 @@ __device__ __forceinline__ bool outward_clear(float cn, float br, float mu, floa
 // heading for a rectangle or a disk get there in one or two events instead
 // of a geometric series of distance budgets: events 552 k -> 446 k per
 // headline frame, -2.5 % frame time (profiles/r02/s22_*).
-__device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B, float a, float perr) {
+// SR_BALL: the budget bounds the displacement from B, not the path. Along
+// the path the direction stays within theta(s) = theta0 + kappa s of the last
+// chord's, so after a path s with theta(s) <= 0.9 the displacement's
+// projection on that direction is at least s cos theta(s) >= s (1 -
+// theta^2 / 2), and it keeps growing over the next chord (at most 1.4 a
+// dphi long, dphi <= 0.071: ball_pw, turning it by at most 8.4 dphi / a <
+// 0.6 more): while every end point stays within Lc (1 - theta(Lc)^2 / 2) of
+// B the path has not reached Lc = min(L, 0.4 a), and r >= a / 2 holds over
+// the path and that chord.
+__device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B, float a, float perr, bool ball_pw) {
     const f3 dv = B - A;
     const f3 nrm_ = ld3(sl.a1);
     const float y = dot(B - ld3(sl.pos), nrm_);
@@ -456,7 +477,14 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     if (!(R > 0.0f)) return 0.0f;
     const float b = c + th0;
     const float L = (__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, 2.0f * kap * R)) - b) * (a2 * (1.0f / 6.06f));
+#if SR_BALL
+    const float Lc = fminf(L, 0.4f * a);
+    const float th = __builtin_fmaf(kap, Lc, th0);
+    return (ball_pw && th < 0.9f) ? Lc * __builtin_fmaf(-0.5f * th, th, 1.0f) * 0.998f : 0.0f;
+#else
+    (void)ball_pw;
     return fminf(L, 0.5f * a) * 0.998f;
+#endif
 }
 // slot j >= 1 for an outward lane at distance a (cyl_par: bs.cm's bit for a budgeted cylinder)
 __device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par, float a, float dip) {
@@ -582,10 +610,33 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #define SR_BH_U 0.986f      // u at r = 1.01420
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
 #define SR_BH_DIP 0.9935f   // 1.0142 x 0.9935 = 1.0076
+#define SR_BALL_PW_DIP 0.99937f  // 1 - 0.071^2 / 8: step angle <= 0.071 (plane_window's displacement form)
+
+// SR_BALL: the step loop's test for the end point X = (cos phi, sin phi) / u
+// of each step (orbital-plane coordinates) against the ball of radius R / 1.01
+// around the centre C: inside when 1 + u (bn cos phi + bt sin phi + Q u) < 0,
+// bn = -2 C.x, bt = -2 C.y, Q = |C|^2 - Rq^2 (that is (|X - C|^2 - Rq^2) u^2).
+// Rq leaves room for the reference's rounding of the chord end point (1.1e-6
+// r, r <= |C| + R), the centre's embedding (nv C.x + tv C.y within 1e-6 |C|
+// of the event's end point and of budget_init's anchor), the frame's
+// non-orthonormality (1e-6 relative) and the test's own float evaluation
+// (below 7 eps (|C| + Rq)^2 in |X - C|^2). +inf: always inside (every budget
+// infinite); -inf, NaN or a ball too small for its margins: never inside.
+__device__ __forceinline__ float ball_q(float R, float cx, float cy) {
+    if (!(R < INFINITY)) return R == INFINITY ? -INFINITY : INFINITY;
+    const float c = fabsf(cx) + fabsf(cy);  // >= |C|
+    const float Rt = R * (1.0f / 1.0101f) - 3.0e-6f * (c + R);
+    if (!(Rt > 0.0f)) return INFINITY;
+    const float s = c + Rt;
+    return __builtin_fmaf(2.0e-6f * s, s, (cx * cx + cy * cy) - Rt * Rt);
+}
 
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     float T, m;
+#if SR_BALL
+    float cx, cy;  // the ball's centre: the last event's end point in the orbital plane (nv, tv)
+#endif
     float uhi;  // the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none)
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
     float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
@@ -636,6 +687,15 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
+#if SR_BALL
+    // the ball's centre: A in the orbital plane (A lies in it: the camera, or a
+    // chord end point), within 1e-6 a of A; the budgets give that up
+    bs.cx = dot(A, nv);
+    bs.cy = dot(A, tv);
+    const float m0 = 2.0e-6f * (a + 1.0f);
+#else
+    const float m0 = 0.0f;
+#endif
     float m = INFINITY;
     budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
     {
@@ -646,13 +706,14 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
             bs.uhi = SR_BH_U;
         }
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
+        e -= m0;
         bs.E[0] = e;
         m = nmin(m, e);
     }
 #pragma unroll 1
     for (int j = 1; j <= nb; j++) {
         const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);  // one batch of scalar loads per slot
-        float e = clearance_obj(sl, A, a);
+        float e = clearance_obj(sl, A, a) - m0;
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
@@ -663,7 +724,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 #pragma unroll
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
         if (c) {
-            const float e = clearance_slab(sc->slots[__builtin_ctz(c)], A, a);
+            const float e = clearance_slab(sc->slots[__builtin_ctz(c)], A, a) - m0;
             bs.E[(bs.slab0 + k) * SR_E_STRIDE] = e;
             mh = nmin(mh, e);
             c &= c - 1;
@@ -930,7 +991,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 float ao = a;
                 asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(B.x), "+v"(B.y), "+v"(B.z));
                 asm volatile("" : "+v"(ao), "+v"(perr));
-                const float w = plane_window(st, A, B, ao, perr);
+                const float w = plane_window(st, A, B, ao, perr, dip > SR_BALL_PW_DIP);
                 v = w > v ? w : v;  // NaN v stays NaN
             }
             if (TY != SR_OBJECT_PLANE && outward &&
@@ -1753,6 +1814,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.i = i;
                 r.steps = sbase + i + 1;
                 settle_prev(i);
+#if SR_BALL
+                // the new orbital plane has its own coordinates: charge the
+                // displacement from the old centre to the chord start r.ro
+                // here, the new chord at the forced event (reseeded)
+                if (CULL)
+                    bs.T = __builtin_fmaf(len(r.ro - (r.nv * bs.cx + r.tv * bs.cy)), 1.0101f,
+                                          3.0e-6f * (fabsf(bs.cx) + fabsf(bs.cy) + 1.0f));
+#endif
                 f3 q;
                 if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
                 r.nv = nrm(q);
@@ -1774,6 +1843,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // Only numbers leave the loop (lane-mask booleans carried out of it
         // cost exec-mask bookkeeping on every step).
         const float lim0 = (every || force) ? -INFINITY : bs.m;
+#if SR_BALL
+        const float bn = CULL ? -2.0f * bs.cx : 0.0f, bt = CULL ? -2.0f * bs.cy : 0.0f;
+        const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bs.m, bs.cx, bs.cy);
+        float vb;  // the step's ball test (< 0: inside)
+#endif
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
         // (bs.cm changes only at reseeds, outside the fast loop)
         const bool any_cm = CULL && __ballot(bs.cm != 0u);
@@ -1794,6 +1868,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             float4 e1 = ldc(tp + 1);
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs cd = CM ? cyl_dirs(sc, bs) : CylDirs{};
+#if SR_BALL
+            const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bs.m, bs.mh), bs.cx, bs.cy)) : q0;
+#endif
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
             if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
@@ -1802,6 +1879,19 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // computed but not applied).
             auto compute = [&]() -> bool {
                 rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
+#if SR_BALL
+                // the end point against the ball (ball_q): a multiply and three FMAs
+                float q = q0;
+                if (CULL && CM) {
+                    rB = __builtin_amdgcn_rcpf(un);
+                    par = chord_parallel(bs.cm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
+                    q = par ? qh : q0;
+                }
+                vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
+                SR_STAT(0, 1);
+                SR_STAT(13, __popcll(__ballot(1)));
+                return __ballot(!(vb < 0.0f) || un < fr.u_f || un > bs.uhi);
+#endif
                 rB = __builtin_amdgcn_rcpf(un);
                 Tn = bs.T;
                 if (CULL) {
@@ -1825,11 +1915,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             };
             // apply step i and move to entry (en, en1) of step i + 1
             auto apply = [&](float4 en, float4 en1) -> bool {
-                bs.T = Tn;
+                if (!SR_BALL) bs.T = Tn;
                 up = r.u;
                 r.u = un;
                 r.du = dun;
-                rA = rB;
+                if (!SR_BALL || CM) rA = rB;
                 tp += 2;
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
@@ -1907,6 +1997,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             Tn = bs.T;
             lim = lim0;
             par = 0;
+#if SR_BALL
+            vb = -1.0f;  // inside every (infinite) budget
+#endif
         };
         if (any_cm) fast(std::true_type{});
         else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
@@ -1924,12 +2017,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return ST_BG;
         }
         const bool bhx = un > bs.uhi;  // the chord left the black hole's u window
+#if SR_BALL
+        const bool event = !(vb < 0.0f) || bhx;
+        if (CULL) {  // the radii of the step's ends (the fast loop carries none)
+            rA = __builtin_amdgcn_rcpf(r.u);
+            rB = __builtin_amdgcn_rcpf(un);
+        }
+#else
         const bool event = !(Tn < lim) || bhx;
         // slots about to run out re-anchor at this event too (within SR_AHEAD
         // of this chord's length plus SR_AHEAD_T of the path since the last
         // event): fewer events, each re-anchoring more
         const float ahead = SR_AHEAD * (Tn - bs.T) + SR_AHEAD_T * Tn;
         bs.T = Tn;
+#endif
         up = r.u;
         r.u = un;
         r.du = dun;
@@ -1947,10 +2048,36 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 const f3 Ap = exact_start ? r.ro : point_near(r, rAold, p1.x, p1.y);
                 const f3 Bp = point_near(r, rB, e.z, e.w);
                 const float pe = point_err(exact_start ? 0.0f : rAold, rB);
+#if SR_BALL
+                // the displacement from the ball's centre to the step's end
+                // point Bp, which becomes the centre: bs.T bounds 1.01 x the
+                // distance between the centres' embeddings and between the
+                // reference's end point and the old centre (the chord is
+                // covered by slot j when bs.T < E[j]: both its ends are in
+                // the ball). After a reseed: the charge from the reseed plus
+                // the chord from the exact r.ro.
+                float ahead;
+                {
+                    const float cx = rB * e.z, cy = rB * e.w;  // Bp = nv cx + tv cy (point_near)
+                    const f3 dv = Bp - Ap;
+                    const float cl = __builtin_amdgcn_sqrtf(dot(dv, dv));
+                    if (reseeded) {
+                        bs.T += (cl * 1.0001f + pe) * SR_PATH_SLACK;
+                    } else {
+                        const float dx = cx - bs.cx, dy = cy - bs.cy;
+                        bs.T = __builtin_fmaf(__builtin_amdgcn_sqrtf(dx * dx + dy * dy), 1.0101f,
+                                              3.0e-6f * (rB + fabsf(bs.cx) + fabsf(bs.cy)));
+                    }
+                    ahead = SR_AHEAD * SR_PATH_SLACK * cl + SR_AHEAD_T * bs.T;
+                    bs.cx = cx;
+                    bs.cy = cy;
+                }
+#else
                 if (reseeded) {  // new frame: the step's bound used the old radius; charge the chord itself
                     const f3 dv = Bp - Ap;
                     bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
                 }
+#endif
                 SR_STAT(1, 1);
 #ifdef SR_STATS
                 r.ev++;
