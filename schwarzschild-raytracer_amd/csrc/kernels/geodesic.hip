@@ -453,14 +453,14 @@ __device__ __forceinline__ bool outward_clear(float cn, float br, float mu, floa
 // headline frame, -2.5 % frame time (profiles/r02/s22_*).
 // SR_BALL: the budget bounds the displacement from B, not the path. Along
 // the path the direction stays within theta(s) = theta0 + kappa s of the last
-// chord's, so after a path s with theta(s) <= 0.9 the displacement's
-// projection on that direction is at least s cos theta(s) >= s (1 -
-// theta^2 / 2), and it keeps growing over the next chord (at most 1.4 a
-// dphi long, dphi <= 0.071: ball_pw, turning it by at most 8.4 dphi / a <
-// 0.6 more): while every end point stays within Lc (1 - theta(Lc)^2 / 2) of
-// B the path has not reached Lc = min(L, 0.4 a), and r >= a / 2 holds over
-// the path and that chord.
-__device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B, float a, float perr, bool ball_pw) {
+// chord's, so the displacement's projection on that direction after a path
+// s is at least the integral of cos theta >= 1 - theta^2 / 2, i.e. s - (th1^3
+// - theta0^3) / (6 kappa) = s (1 - (th1^2 + th1 theta0 + theta0^2) / 6) with
+// th1 = theta(s), and it grows while theta < pi / 2. The first end point past
+// a path Lc is at most one chord further (<= 1.5 a dphi: r <= 1.5 a): with
+// Lc capped so that r >= a / 2 (kappa's bound) and theta <= 1.5 still hold
+// there, an end point within that projection bound of B has a path below Lc.
+__device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B, float a, float perr, float dphi) {
     const f3 dv = B - A;
     const f3 nrm_ = ld3(sl.a1);
     const float y = dot(B - ld3(sl.pos), nrm_);
@@ -478,11 +478,13 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     const float b = c + th0;
     const float L = (__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, 2.0f * kap * R)) - b) * (a2 * (1.0f / 6.06f));
 #if SR_BALL
-    const float Lc = fminf(L, 0.4f * a);
-    const float th = __builtin_fmaf(kap, Lc, th0);
-    return (ball_pw && th < 0.9f) ? Lc * __builtin_fmaf(-0.5f * th, th, 1.0f) * 0.998f : 0.0f;
+    const float ch = 1.5f * a * dphi;  // the next chord
+    const float Lc = fminf(L, fminf(__builtin_fmaf(0.5f, a, -ch), (1.5f - th0) * (a2 * (1.0f / 6.06f)) - ch));
+    const float th1 = __builtin_fmaf(kap, Lc, th0);
+    const float f = 1.0f - (th1 * th1 + th1 * th0 + th0 * th0) * (1.0f / 6.0f);
+    return (Lc > 0.0f && f > 0.0f) ? Lc * f * 0.998f : 0.0f;
 #else
-    (void)ball_pw;
+    (void)dphi;
     return fminf(L, 0.5f * a) * 0.998f;
 #endif
 }
@@ -610,7 +612,6 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #define SR_BH_U 0.986f      // u at r = 1.01420
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
 #define SR_BH_DIP 0.9935f   // 1.0142 x 0.9935 = 1.0076
-#define SR_BALL_PW_DIP 0.99937f  // 1 - 0.071^2 / 8: step angle <= 0.071 (plane_window's displacement form)
 
 // SR_BALL: the step loop's test for the end point X = (cos phi, sin phi) / u
 // of each step (orbital-plane coordinates) against the ball of radius R / 1.01
@@ -953,6 +954,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     SR_PTB(3);
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
+    const float dphi = __builtin_amdgcn_sqrtf(8.0f * (1.0f - dip));  // >= the step angle (sr_dev_frame.out_dip)
     uint32_t reach = 0;
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
@@ -991,7 +993,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 float ao = a;
                 asm volatile("" : "+v"(A.x), "+v"(A.y), "+v"(A.z), "+v"(B.x), "+v"(B.y), "+v"(B.z));
                 asm volatile("" : "+v"(ao), "+v"(perr));
-                const float w = plane_window(st, A, B, ao, perr, dip > SR_BALL_PW_DIP);
+                const float w = plane_window(st, A, B, ao, perr, dphi);
                 v = w > v ? w : v;  // NaN v stays NaN
             }
             if (TY != SR_OBJECT_PLANE && outward &&
