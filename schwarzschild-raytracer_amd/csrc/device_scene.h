@@ -120,6 +120,10 @@ typedef struct {
     sr_dev_slot slots[SR_MAX_BUDGET];  // budget slots 1..num_budget
     int32_t num_step;         // objects of SR_KIND_EXACT / SR_KIND_CHORD (tested every step)
     int32_t step_idx[SR_MAX_OBJECTS];
+    // an unbounded ray (the flat intersect, frag:895-897) from beyond this
+    // radius squared that does not approach the origin misses every object
+    // and the black hole (+inf: planes or unbounded objects)
+    float flat_miss_r2;
     float tr_curved_color[4];
     float tr_flat_color[4];
     float tr_flat[SR_SEG_FLOATS];  // flat test-ray cylinder

@@ -1717,6 +1717,19 @@ __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, f
 #endif
 }
 
+// The flat intersect of a ray that left the u_f sphere (frag:895-897,
+// 903-905) when it provably hits nothing: from ro beyond sc->flat_miss_r2
+// (twice the reach of every object's acceptance region and the black hole,
+// plus one) and not approaching the origin (ro . rd >= 0, within rounding
+// far below that factor), every point of the ray is at least |ro| from the
+// origin. Its colour is then get_bg(rd) alone (intersect adds vec4(0), frag
+// is never -0), exactly ST_BG's: the shade kernel skips the exhaustive
+// intersect, and the hand-off the ray origin (1.65 M of the headline frame's
+// 2.07 M pixels end this way).
+__device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc, f3 ro, f3 rd) {
+    return !sc->tr_visible && dot(ro, rd) >= 0.0f && dot(ro, ro) > sc->flat_miss_r2;
+}
+
 // The step loop, frag:890-933, from step r.i (entry: r.u = u after step
 // r.i - 1, r.ro / r.rd = that step's chord end and direction).
 //
@@ -1825,9 +1838,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                                           3.0e-6f * (fabsf(bs.cx) + fabsf(bs.cy) + 1.0f));
 #endif
                 f3 q;
-                if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q)) return ST_FLAT;
+                if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q))
+                    return flat_misses(sc, r.ro, r.rd) ? ST_BG : ST_FLAT;
                 r.nv = nrm(q);
-                if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return ST_FLAT;
+                if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return flat_misses(sc, r.ro, r.rd) ? ST_BG : ST_FLAT;
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
                 r.u = 1.0f / len(q);
                 r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
@@ -2300,6 +2314,12 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST>(sc, segs, tbl, fr, tx, r, hit, log);
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
+#if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
+        // pixels, logged hits, pixels by status (tools/stats_frame.py; wave sums)
+        SR_STAT(23, __popcll(__ballot(1)));
+        SR_STAT(24, __popcll(__ballot(log.n & 1)) + 2 * __popcll(__ballot(log.n & 2)) + 4 * __popcll(__ballot(log.n & 4)));
+        for (int k = 0; k < 6; k++) SR_STAT(25 + k, __popcll(__ballot(st == k)));
+#endif
         if (st == ST_FLAT || st == ST_MORE) ps.put3(PS_RO, id, r.ro);
         if (st == ST_MORE) {  // resumable (sr_resume_kernel)
             ps.puti(PS_I, id, r.i);

@@ -744,6 +744,7 @@ int sr_create(sr_ctx** out, int hip_device) {
     if (!c) return SR_E_NOMEM;
     c->device = hip_device;
     std::memset(&c->h_scene, 0, sizeof c->h_scene);
+    c->h_scene.flat_miss_r2 = INFINITY;  // set by sr_set_scene
     if (!hip_ok(hipStreamCreateWithFlags(&c->upload, hipStreamNonBlocking))) {
         c->upload = nullptr;
         sr_destroy(c);
@@ -901,6 +902,21 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
         } else {
             d.step_idx[d.num_step++] = i;
         }
+    }
+    {  // the flat intersect's far-field miss radius (geodesic.hip flat_misses)
+        double R = 1.0 + SR_MU_QUADRATIC * 3.0;  // the black hole
+        for (int i = 0; i < s->num_objects && std::isfinite(R); i++) {
+            const sr_dev_obj& o = d.objs[i];
+            const double bc = std::sqrt((double)o.bc[0] * o.bc[0] + (double)o.bc[1] * o.bc[1] + (double)o.bc[2] * o.bc[2]);
+            if (o.kind == SR_KIND_EXACT || o.type == SR_OBJECT_PLANE || !std::isfinite(o.br) || !std::isfinite(bc))
+                R = INFINITY;
+            else
+                R = std::max(R, bc + (double)o.br);
+        }
+        // beyond twice that plus one, with a margin far above any rounding of
+        // the tests' quadratics and slab distances at that range
+        const double r = 2.0 * R + 1.0;
+        d.flat_miss_r2 = std::isfinite(r) ? std::nextafter((float)(r * r), INFINITY) : INFINITY;
     }
     std::memcpy(d.materials, s->materials, sizeof d.materials);
     std::memcpy(d.lights, s->lights, sizeof d.lights);

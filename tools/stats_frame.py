@@ -56,6 +56,9 @@ def main():
         return f"slot{k - 2}_reached" if 2 <= k <= 10 else f"slot{k - 14}_spent"
 
     out = {name(k): int(buf[k]) for k in range(23)}
+    # the hand-off (plain SR_STATS builds): pixels, logged hit records, pixels by status
+    out["handoff"] = {"pixels": int(buf[23]), "hit_records": int(buf[24]),
+                      **{n: int(buf[25 + k]) for k, n in enumerate(["done", "hit", "more", "flat", "bg", "bh"])}}
     out["event_frac"] = out["events"] / max(1, out["wave_steps"])
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
