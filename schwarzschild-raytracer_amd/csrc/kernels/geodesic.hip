@@ -98,7 +98,7 @@ struct Tex {
 // Measurement builds only: wave-level event counters (tools/stats_frame.py).
 //   0 wave-steps  1 budget events  2..10 slot j reached (exact chord)
 //   11 -  12 exact object tests run  13 lane-steps  14..22 slot j spent
-__device__ unsigned long long sr_stats[32];
+__device__ unsigned long long sr_stats[64];
 // per-wave [start, end] s_memrealtime (100 MHz) of sr_integrate_kernel, by wave index
 #define SR_WAVE_LOG (1 << 17)
 #define SR_WAVE_REC 16  // t0, t1, max steps, events << 32 | exact chords, reach count of slots 0..8
@@ -1811,6 +1811,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     };
     bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
     int i = r.i;
+#ifdef SR_STATS
+    int last_ev = i;
+#endif
 #ifdef SR_PROF
     unsigned prof_t_ = (unsigned)clock64();
     bs.prof = r.prof;
@@ -2097,6 +2100,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_STAT(1, 1);
 #ifdef SR_STATS
                 r.ev++;
+                {  // steps since the wave's previous event, lanes that triggered it (tools/stats_frame.py)
+                    const int iv = i - last_ev;
+                    last_ev = i;
+                    SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
+                    const int nl = __popcll(__ballot(event));
+                    SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
+#if SR_BALL
+                    if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
+#endif
+                }
 #endif
                 // sr_wave_costs: the wave's event count (one lane, its own LDS word)
                 if (WCOST && (int)__lane_id() == __builtin_ctzll(__ballot(1)))
@@ -2639,6 +2652,16 @@ extern "C" int sr_debug_stats(unsigned long long* out32) {
     if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
     unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z) != hipSuccess) return -3;
+    return 0;
+}
+// counters 32..63 (read and cleared): event intervals and triggering lanes
+extern "C" int sr_debug_stats_hi(unsigned long long* out32) {
+    if (hipDeviceSynchronize() != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long), 32 * sizeof(unsigned long long)) !=
+        hipSuccess)
+        return -3;
+    unsigned long long z[32] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z, 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
     return 0;
 }
 extern "C" int sr_debug_wave_times(unsigned long long* out, int n_waves) {

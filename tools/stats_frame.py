@@ -48,6 +48,10 @@ def main():
     ra, rb = args.rows
     r.render(cam, params, 1920, 1080, ra, rb)  # first frame: centre-out launch order
     lib.sr_debug_stats(buf)  # clear
+    if hasattr(lib, "sr_debug_stats_hi"):
+        lib.sr_debug_stats_hi.restype = C.c_int
+        lib.sr_debug_stats_hi.argtypes = [C.POINTER(C.c_ulonglong)]
+        lib.sr_debug_stats_hi((C.c_ulonglong * 32)())  # clear
     r.render(cam, params, 1920, 1080, ra, rb)  # steady state: cost-ordered launch
     assert lib.sr_debug_stats(buf) == 0
     def name(k):
@@ -60,6 +64,14 @@ def main():
     out["handoff"] = {"pixels": int(buf[23]), "hit_records": int(buf[24]),
                       **{n: int(buf[25 + k]) for k, n in enumerate(["done", "hit", "more", "flat", "bg", "bh"])}}
     out["event_frac"] = out["events"] / max(1, out["wave_steps"])
+    if hasattr(lib, "sr_debug_stats_hi"):  # counters 32..63 of the same frame
+        hi = (C.c_ulonglong * 32)()
+        lib.sr_debug_stats_hi.restype = C.c_int
+        lib.sr_debug_stats_hi.argtypes = [C.POINTER(C.c_ulonglong)]
+        assert lib.sr_debug_stats_hi(hi) == 0
+        out["event_interval_steps"] = dict(zip(["1", "2-3", "4-7", "8-15", "16-63", "64+"], [int(hi[k]) for k in range(6)]))
+        out["event_trigger_lanes"] = dict(zip(["1", "2-3", "4-7", "8-15", "16-31", "32+"], [int(hi[6 + k]) for k in range(6)]))
+        out["events_bh_window_only"] = int(hi[12])
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
 
