@@ -340,7 +340,7 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // no chord can come within the per-chord acceptance region of slot j and its
 // exact test cannot hit: it is skipped. clearance_j(A) is
 //     max(|A - c| - rb, |n.(A - pos)| - mp)  (planar objects: the plane bound)
-//     - 1.8 mu_q |A|                         (chord origins |o|_1 <= 1.8 (|A| + T))
+//     - 1.8 mu |A|                           (chord origins |o|_1 <= 1.8 (|A| + T); mu = slot_mu)
 // with rb = bounding radius + mu_q (1 + |c|_1 + R) and the path slack covering
 // the T-proportional part of the rounding margins. Cylinders also subtract
 // their quadratic margin SR_CYL_QMARGIN S^2 / (r SR_BUDGET_DPMIN) for the
@@ -364,6 +364,13 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 #ifndef SR_NEAR
 #define SR_NEAR 1.0f
 #endif
+// The margin factor of a slot's distance tests: a planar primitive's
+// per-chord factor (SR_MU_PLANAR: it accepts a chord point within a few eps
+// S of its plane and bounds), the quadratic one for spheres and cylinders
+// (sr_api.cpp set_bound; the slab and in-plane margins sl.mp use the same).
+__device__ __forceinline__ float slot_mu(const sr_dev_slot& sl) {
+    return sl.type == SR_OBJECT_CYLINDER ? SR_MU_QUADRATIC : sl.mu;
+}
 __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, float a) {
     float c;
     {
@@ -411,7 +418,7 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
             c = fminf(c - qm, SR_BUDGET_TMAX);
         }
     }
-    return c - 1.8f * SR_MU_QUADRATIC * a;
+    return c - 1.8f * slot_mu(sl) * a;
 }
 // black hole: sphere_test accepts only its entry or exit point, on the r = 1
 // shell (a ray can cross the shell between steps and go on inside)
@@ -472,7 +479,7 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     const float kap = 6.06f * __builtin_amdgcn_rcpf(a2);  // 6 / a^2 plus 1 %
     const float c = (y > 0.0f ? -1.0f : 1.0f) * dot(dv, nrm_) * il;
     const float th0 = __builtin_fmaf(kap, len, __builtin_fmaf(2.0f * perr, il, 1e-4f));
-    const float m = (sl.mp + SR_MU_QUADRATIC * __builtin_fmaf(3.1f, a, 1.0f)) * 1.001f + perr;  // S <= 3.1 a + 1
+    const float m = (sl.mp + sl.mu * __builtin_fmaf(3.1f, a, 1.0f)) * 1.001f + perr;  // S <= 3.1 a + 1 (planar)
     const float R = fabsf(y) - m;
     if (!(R > 0.0f)) return 0.0f;
     const float b = c + th0;
@@ -794,7 +801,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
         c = ld3(sl.bc);
         R = sl.br + sl.mu * S;
         if (sl.mp < INFINITY) {  // orthonormal frame: tighter regions than the bounding sphere
-            const float m = (sl.mp + SR_MU_QUADRATIC * S) * 1.001f + perr;
+            const float m = (sl.mp + slot_mu(sl) * S) * 1.001f + perr;
             const f3 pos = ld3(sl.pos);
             const f3 a1 = ld3(sl.a1);
             const float yA = dot(A - pos, a1), yB = dot(B - pos, a1);
@@ -1442,16 +1449,22 @@ __device__ __forceinline__ int hit_opacity_uniform(const sr_dev_scene* __restric
     if (m.invert_uv_x) uv.x = 1.0f - uv.x;
     if (m.invert_uv_y) uv.y = 1.0f - uv.y;
     const int ti = m.texture_index < SR_MAX_TEXTURES ? m.texture_index : 0;
-    f2 r = F2((uv.x * sc->texture_sizes[ti][0]) / sc->max_texture_size[0],
-              (uv.y * sc->texture_sizes[ti][1]) / sc->max_texture_size[1]);
+    // the sizes pinned here: hoisted out of the step loop (their float
+    // conversions, the divisors' scalings and the wrap's magic reciprocals)
+    // they stayed live across it and were spilled
+    float tsx = sc->texture_sizes[ti][0], tsy = sc->texture_sizes[ti][1];
+    float msx = sc->max_texture_size[0], msy = sc->max_texture_size[1];
+    int aw = fr.arr_w, ah = fr.arr_h;
+    asm volatile("" : "+s"(tsx), "+s"(tsy), "+s"(msx), "+s"(msy), "+s"(aw), "+s"(ah));
+    f2 r = F2((uv.x * tsx) / msx, (uv.y * tsy) / msy);
     int layer = m.texture_index;
     if (layer > fr.arr_layers - 1) layer = fr.arr_layers - 1;
-    const float s = r.x * (float)fr.arr_w - 0.5f;  // bilinear()
-    const float t = r.y * (float)fr.arr_h - 0.5f;
+    const float s = r.x * (float)aw - 0.5f;  // bilinear()
+    const float t = r.y * (float)ah - 0.5f;
     if (!(fabsf(s) < 4194304.0f) || !(fabsf(t) < 4194304.0f)) return OP_MAYBE;
-    const int x = wrap_rep(floorf(s), fr.arr_w), y = wrap_rep(floorf(t), fr.arr_h);
-    const size_t stride = ((size_t)fr.arr_w + 7) >> 3;
-    const uint8_t bits = tx.opq[((size_t)layer * (size_t)fr.arr_h + (size_t)y) * stride + (size_t)(x >> 3)];
+    const int x = wrap_rep(floorf(s), aw), y = wrap_rep(floorf(t), ah);
+    const size_t stride = ((size_t)aw + 7) >> 3;
+    const uint8_t bits = tx.opq[((size_t)layer * (size_t)ah + (size_t)y) * stride + (size_t)(x >> 3)];
     return (bits >> (x & 7)) & 1 ? OP_OPAQUE : OP_MAYBE;
 }
 
@@ -2108,6 +2121,27 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
 #if SR_BALL
                     if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
+                    SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
+                    SR_STAT(46, __popcll(__ballot(bhx)));
+                    SR_STAT(47, nl);
+                    if (iv <= 1) {
+                        SR_STAT(48, nl >= 32);
+                        SR_STAT(49, __popcll(__ballot(event && !(q0 < INFINITY))));
+                        SR_STAT(50, nl);
+                        SR_STAT(51, __popcll(__ballot(event && reseeded)));
+                        SR_STAT(52, __popcll(__ballot(event && bs.m < 0.05f)));
+                        SR_STAT(53, any_cm);
+                        {  // the slot holding the smallest budget of each triggering lane
+                            int jm = 0;
+                            float em = bs.E[0];
+                            for (int j = 1; j <= sc->num_budget; j++) {
+                                const float v = bs.E[j * SR_E_STRIDE];
+                                if (v < em) { em = v; jm = j; }
+                            }
+                            for (int j = 0; j <= 8; j++) SR_STAT(55 + j, __popcll(__ballot(event && jm == j && em < 0.05f)));
+                        }
+                    }
+                    SR_STAT(54, any_cm);
 #endif
                 }
 #endif

@@ -153,9 +153,12 @@ void set_bound(sr_dev_obj& o, V3 c, float R, int kind, float mu) {
     V3 n = ld(o.f + SR_F_AXES + 3);
     bool typed = o.type == SR_OBJECT_DISK || o.type == SR_OBJECT_HOLLOW_DISK || o.type == SR_OBJECT_RECTANGLE ||
                  o.type == SR_OBJECT_BOX || o.type == SR_OBJECT_CYLINDER;
-    o.mp = typed && std::fabs(dot(n, n) - 1.f) < 1e-5f
-               ? SR_MU_QUADRATIC * (1.f + l1norm(ld(o.f + SR_F_POS)) + R)
-               : INFINITY;
+    // Planar primitives (disks, annuli, rectangles, box faces) accept a point
+    // of the chord within a few eps S of the plane and of their in-plane
+    // bounds, so their per-chord factor (SR_MU_PLANAR, ~100x that) serves
+    // here too; the cylinder's height and radius keep the quadratic one.
+    const float md = o.type == SR_OBJECT_CYLINDER ? SR_MU_QUADRATIC : mu;
+    o.mp = typed && std::fabs(dot(n, n) - 1.f) < 1e-5f ? md * (1.f + l1norm(ld(o.f + SR_F_POS)) + R) : INFINITY;
     o.pl1 = l1norm(ld(o.f + SR_F_POS));
 }
 

@@ -72,6 +72,11 @@ def main():
         out["event_interval_steps"] = dict(zip(["1", "2-3", "4-7", "8-15", "16-63", "64+"], [int(hi[k]) for k in range(6)]))
         out["event_trigger_lanes"] = dict(zip(["1", "2-3", "4-7", "8-15", "16-31", "32+"], [int(hi[6 + k]) for k in range(6)]))
         out["events_bh_window_only"] = int(hi[12])
+        out["event_lanes"] = {k: int(hi[13 + n]) for n, k in enumerate(
+            ["empty_ball", "bh_window", "triggered", "interval1_events_32plus", "interval1_empty_ball",
+             "interval1_triggered", "interval1_reseeded", "interval1_budget_below_0.05", "interval1_cm_events",
+             "cm_events"])}
+        out["interval1_small_budget_lanes_by_slot"] = [int(hi[23 + j]) for j in range(9)]
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
 
