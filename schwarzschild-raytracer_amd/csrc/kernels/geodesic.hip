@@ -618,6 +618,25 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #endif
 #define SR_BH_U 0.986f      // u at r = 1.01420
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
+// The inner window (SR_BH_WINDOW2): chords whose two ends both lie at r in
+// [1.00402, 1.1] (u in [SR_BH_ULO2, SR_BH_U2]) with a step angle below 0.063
+// (out_dip > SR_BH_DIP2) stay at least 1.00402 x 0.9995 = 1.00352 from the
+// origin. sphere_test computes their discriminant within 12 eps (|o|^2 + 1)
+// <= 1.6e-6 (|o| <= 1.1), so a root it accepts lies within sqrt(1.6e-6) =
+// 1.26e-3 of a true root (near tangency; less elsewhere), while the segment
+// ends at least 3.5e-3 from the sphere along the line: none is accepted. A
+// lane there needs no distance budget for the hole either; the step loop
+// exits on u > SR_BH_U2 or u < SR_BH_ULO2 (climbing past r = 1.1; the u_f
+// compare, per lane). Rays falling in crossed the band r < 1.0142 with an
+// event on every step (their distance budget was below one step).
+#ifndef SR_BH_WINDOW2
+#define SR_BH_WINDOW2 1
+#endif
+#define SR_BH_U2 0.996f       // u at r = 1.004016
+#define SR_BH_ULO2 0.90910f   // u at r = 1.09999
+#define SR_BH_RWIN2 1.00403f  // an anchor beyond this radius (by perr) ...
+#define SR_BH_RMAX2 1.0999f   // ... and within this one starts an inner window
+#define SR_BH_DIP2 0.9995f
 #define SR_BH_DIP 0.9935f   // 1.0142 x 0.9935 = 1.0076
 
 // SR_BALL: the step loop's test for the end point X = (cos phi, sin phi) / u
@@ -645,7 +664,9 @@ struct Budget {
 #if SR_BALL
     float cx, cy;  // the ball's centre: the last event's end point in the orbital plane (nv, tv)
 #endif
-    float uhi;  // the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none)
+    float uhi;  // the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; SR_BH_U2:
+                // the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo())
+    __device__ __forceinline__ float ulo(float u_f) const { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
     uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
     float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
                   // covers chords nearly parallel to an axis
@@ -691,7 +712,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 }
 
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv,
-                                            bool outward, float dip, bool bh_ok) {
+                                            bool outward, float dip, bool bh_ok, bool falling) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.T = 0.0f;
@@ -712,6 +733,10 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         if (SR_BH_WINDOW && bh_ok && a > SR_BH_RWIN) {
             e = INFINITY;
             bs.uhi = SR_BH_U;
+        }
+        if (SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a > SR_BH_RWIN2 && a < SR_BH_RMAX2 && (falling || !(a > SR_BH_RWIN))) {
+            e = INFINITY;
+            bs.uhi = SR_BH_U2;
         }
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
         e -= m0;
@@ -874,7 +899,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // tests; all lanes re-anchor those.
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
-                                                 bool outward, float dip, bool bhx, bool bh_ok) {
+                                                 bool outward, float dip, bool bhx, bool bh_ok, bool falling) {
     constexpr int NS = SR_MAX_BUDGET + 1;
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -974,8 +999,11 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         const bool h = (hard >> j) & 1u;
         if (j == 0) {
             // beyond the band: the u window instead of a distance budget
-            const bool win = SR_BH_WINDOW && bh_ok && a - perr > SR_BH_RWIN;
-            bs.uhi = win ? SR_BH_U : INFINITY;
+            const bool win1 = SR_BH_WINDOW && bh_ok && a - perr > SR_BH_RWIN;
+            const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a - perr > SR_BH_RWIN2 && a + perr < SR_BH_RMAX2 &&
+                              (falling || !win1);
+            const bool win = win1 || win2;
+            bs.uhi = win2 ? SR_BH_U2 : win1 ? SR_BH_U : INFINITY;
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
@@ -1777,7 +1805,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     bs.uhi = INFINITY;
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP);
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -1875,6 +1903,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // Only numbers leave the loop (lane-mask booleans carried out of it
         // cost exec-mask bookkeeping on every step).
         const float lim0 = (every || force) ? -INFINITY : bs.m;
+        const float ulo = bs.ulo(fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
 #if SR_BALL
         const float bn = CULL ? -2.0f * bs.cx : 0.0f, bt = CULL ? -2.0f * bs.cy : 0.0f;
         const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bs.m, bs.cx, bs.cy);
@@ -1922,7 +1951,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
-                return __ballot(!(vb < 0.0f) || un < fr.u_f || un > bs.uhi);
+                return __ballot(!(vb < 0.0f) || un < ulo || un > bs.uhi);
 #endif
                 rB = __builtin_amdgcn_rcpf(un);
                 Tn = bs.T;
@@ -2007,7 +2036,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(0, 1);
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
-                    if (__ballot(un < fr.u_f || un > bs.uhi)) {
+                    if (__ballot(un < ulo || un > bs.uhi)) {
 #pragma unroll
                         for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
@@ -2048,7 +2077,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             settle_prev(i);
             return ST_BG;
         }
-        const bool bhx = un > bs.uhi;  // the chord left the black hole's u window
+        // the chord left the black hole's u window (or the inner one outward)
+        const bool bhx = un > bs.uhi || (un < SR_BH_ULO2 && bs.uhi == SR_BH_U2);
 #if SR_BALL
         const bool event = !(vb < 0.0f) || bhx;
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
@@ -2187,7 +2217,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                     bhx, fr.win_ok && fr.out_dip > SR_BH_DIP);
+                                     bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
