@@ -191,6 +191,9 @@ typedef struct {
     // 1: every chord origin lies within r = 100 (u_f >= 0.01 and the cameras
     // inside), where the black hole's u window holds (geodesic.hip SR_BH_WINDOW)
     int32_t win_ok;
+    // the scene's budget slots (sr_dev_scene.num_budget): picks the integrate
+    // kernel's slot capacity (geodesic.hip SR_NB_SMALL)
+    int32_t num_budget;
 } sr_dev_frame;
 
 #endif

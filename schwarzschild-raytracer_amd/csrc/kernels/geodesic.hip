@@ -897,10 +897,11 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // slot capacity, no per-slot branches or LDS round trips), then only the
 // slots some lane has spent - usually one - run their clearance and reach
 // tests; all lanes re-anchor those.
+template <int NB>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, bool bhx, bool bh_ok, bool falling) {
-    constexpr int NS = SR_MAX_BUDGET + 1;
+    constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
     const float T = bs.T;
@@ -1793,7 +1794,7 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 // sr_wave_costs: budget events of each wave of the integrate kernel's workgroup
 __shared__ int sr_lds_ev[SR_WG / 64];
 
-template <bool CULL, bool RECORD, bool WCOST = false>
+template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
@@ -2216,7 +2217,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
-                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                reach = budget_event<NB>(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
                 SR_PT(6);
 #ifdef SR_STATS
@@ -2299,6 +2300,9 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #ifndef SR_MIN_WAVES_PER_EU
 #define SR_MIN_WAVES_PER_EU 6
 #endif
+#ifndef SR_NB_SMALL
+#define SR_NB_SMALL 6
+#endif
 
 // Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
 // tile << 8 | SR_SPLIT | sub for workgroup `sub` of a split tile; -1 for an
@@ -2331,7 +2335,10 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // the tile's cost (max steps of its rays over the batch).
 // WCOST: the sr_wave_costs instantiation (per-wave steps and events to
 // fr.wave_cost); the frame kernels carry none of its code.
-template <bool CULL, bool WCOST = false>
+// NB: budget slots the event path handles (>= the scene's sc->num_budget;
+// sr_launch_geodesic picks SR_NB_SMALL when it suffices: the default scene
+// has six, and phase 1 of an event runs over every slot of the capacity).
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET>
 __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
@@ -2389,7 +2396,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
-        if (st < 0) st = integrate<CULL, true, WCOST>(sc, segs, tbl, fr, tx, r, hit, log);
+        if (st < 0) st = integrate<CULL, true, WCOST, NB>(sc, segs, tbl, fr, tx, r, hit, log);
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
         // pixels, logged hits, pixels by status (tools/stats_frame.py; wave sums)
@@ -2668,6 +2675,9 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (cull && fr->num_budget <= SR_NB_SMALL)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
+                           dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (cull)
         hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
                            tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);

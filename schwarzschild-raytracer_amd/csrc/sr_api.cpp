@@ -652,6 +652,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     for (int f = 1; f < n_frames; f++) build_cam(&cams[f], fr.cam[f]);
     fr.batch = n_frames;
     // the black hole's u window (geodesic.hip SR_BH_WINDOW): chord origins within r = 100
+    fr.num_budget = ctx->h_scene.num_budget;
     fr.win_ok = fr.uf_radius <= 100.5f;
     for (int f = 0; f < n_frames; f++) {
         const float* q = fr.cam[f].pos;

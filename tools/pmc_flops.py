@@ -63,7 +63,7 @@ def calib_factors(root):
     return rows
 
 
-def frame_counters(roots, kernel="sr_integrate_kernel<true, false>"):
+def frame_counters(roots, kernel="sr_integrate_kernel<true, false"):
     per = collections.defaultdict(list)
     grids = collections.Counter()
     recs = []
@@ -133,7 +133,7 @@ def main():
     flop = c.get("SQ_INSTS_VALU_FLOPS_FP32", 0.0) * k_flop  # transcendentals included (1 each)
     trans = c.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0.0) * k_trans
     rec = {
-        "kernel": "sr_integrate_kernel<true, false>",
+        "kernel": "sr_integrate_kernel<true, false, NB>",
         "kernel_sha": bench.kernel_sha(),
         "width": args.width,
         "height": args.height,

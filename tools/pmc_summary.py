@@ -7,7 +7,7 @@ import json
 import sys
 
 
-def summarise(root, kernel="sr_integrate_kernel<true, false>"):
+def summarise(root, kernel="sr_integrate_kernel<true, false"):
     out = {}
     for p in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         agg = collections.defaultdict(float)

@@ -24,7 +24,7 @@ def main():
     a = ap.parse_args()
     rows = []
     for p in glob.glob(f"{a.run}/**/*kernel_trace.csv", recursive=True):
-        rows += [r for r in csv.DictReader(open(p)) if "sr_integrate_kernel<true, false>" in r["Kernel_Name"]]
+        rows += [r for r in csv.DictReader(open(p)) if "sr_integrate_kernel<true, false" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
     B, F = 1, 4

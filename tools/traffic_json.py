@@ -35,7 +35,7 @@ def main():
     fetch = c["FETCH_SIZE"] * 1024.0
     write = c["WRITE_SIZE"] * 1024.0
     rec = {
-        "kernel": "sr_integrate_kernel<true, false>",
+        "kernel": "sr_integrate_kernel<true, false, NB>",
         "kernel_sha": bench.kernel_sha(),
         "width": a.width, "height": a.height, "max_steps": a.max_steps,
         "fetch_bytes_raw": fetch, "fetch_bytes_x2_bound": 2 * fetch, "write_bytes": write,
