@@ -987,7 +987,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     SR_PTB(3);
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
-    const float dphi = __builtin_amdgcn_sqrtf(8.0f * (1.0f - dip));  // >= the step angle (sr_dev_frame.out_dip)
+    float dipv = dip;
+    asm volatile("" : "+v"(dipv));  // computed here: hoisted out of the step loop it was a spilled VGPR
+    const float dphi = __builtin_amdgcn_sqrtf(8.0f * (1.0f - dipv));  // >= the step angle (sr_dev_frame.out_dip)
     uint32_t reach = 0;
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
@@ -1688,10 +1690,14 @@ __device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const sr_dev_c
 }
 
 // Where integrate() records translucent hits (sr_integrate_kernel only)
+// The integrate kernel's pixel ids, one LDS word per thread: read where a hit
+// is logged and at the hand-off, not held in registers across the step loop
+// (a 64-bit id there was spilled to scratch for the whole loop).
+__shared__ uint32_t sr_lds_pid[SR_WG];
 struct HitLog {
     PS ps;
-    size_t id;
     int n;
+    __device__ __forceinline__ size_t id() const { return (size_t)sr_lds_pid[threadIdx.x]; }
 };
 
 // Chord end point of step j, frag:924: (nv cos phi_j + tv sin phi_j) / u_j
@@ -2251,7 +2257,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 // r.steps: the ray's step count if this hit ends it
                 // the whole 32-byte sector in two 16-byte stores (a partial
                 // sector costs a read-modify-write)
-                float4* h = reinterpret_cast<float4*>(log.ps.hit(log.id, log.n));
+                float4* h = reinterpret_cast<float4*>(log.ps.hit(log.id(), log.n));
                 h[0] = make_float4(hit.p.x, hit.p.y, hit.p.z,
                                    __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (r.steps << 8)));
                 h[1] = make_float4(r.rd.x, r.rd.y, r.rd.z, 0.0f);
@@ -2380,12 +2386,12 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #endif
     if (WCOST && (threadIdx.x & 63) == 0) sr_lds_ev[threadIdx.x >> 6] = 0;
     if (tid >= 0 && pixel_of(fr, block, tid, q)) {
-        const size_t id = ((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256 + tid;
+        sr_lds_pid[threadIdx.x] = (uint32_t)(((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256 + tid);
         Tex tx;
         tx.bg = nullptr;
         tx.arr = arr;
         tx.opq = opq;
-        HitLog log{PS{ps_base, ps_n}, id, 0};
+        HitLog log{PS{ps_base, ps_n}, 0};
         const PS& ps = log.ps;
         Ray r;
         Hit hit;
@@ -2397,6 +2403,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST, NB>(sc, segs, tbl, fr, tx, r, hit, log);
+        const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
         // pixels, logged hits, pixels by status (tools/stats_frame.py; wave sums)
@@ -2629,7 +2636,7 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         r.du = ps.at(PS_DU, id);
         r.i = ps.geti(PS_I, id) + 1;
         r.steps = (int)((unsigned)__float_as_int(rec.x) >> 8);
-        HitLog log{ps, (size_t)id, 0};
+        HitLog log{ps, 0};  // RECORD = false: nothing is logged
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();
             const int st = integrate<CULL, false>(sc, segs, tbl, fr, tx, r, hit, log);
