@@ -152,7 +152,12 @@ def parse():
     ap.add_argument("--reference-loop", choices=["on", "off"], default="on",
                     help="time one un-culled frame (the reference's per-step all-object loop) for "
                          "roofline.speedup_vs_reference_loop")
-    ap.add_argument("--cpu-sample-rows", type=int, default=0, help="rows of the frame swept on the CPU (0 = auto)")
+    ap.add_argument("--cpu-sample-rows", type=int, default=0,
+                    help="rows of the frame swept on the CPU for `value` (0 = every row: the full frame)")
+    ap.add_argument("--single-frame", choices=["on", "off"], default="on",
+                    help="also time single-frame launches (N = 1): one frame alone, and 4 in flight")
+    ap.add_argument("--single-split", default="0",
+                    help="split tiles for the single-frame figures: max_tiles[:lanes[:min_steps]] (0 = off)")
     ap.add_argument("--dump-frames", default="",
                     help="directory: rank 0 saves every timed frame as assembled (frame_<f>.npy), for the "
                          "multi-rank parity test; copies are taken after the timed region")
@@ -254,7 +259,8 @@ def main():
     def keep(first, batch):
         if batch is None:
             return
-        last[0] = (first, batch)
+        # FrameGather reuses its frame buffer at its next call: keep a copy
+        last[0] = (first, batch.clone() if hasattr(batch, "clone") else batch)
         if args.dump_frames:
             for i in range(batch.shape[0]):
                 if first + i >= dump_from[0]:
@@ -430,6 +436,15 @@ def main():
     torch.cuda.synchronize(dev)
     latency_ms = ev0.elapsed_time(ev1) / lat_launches
 
+    # Single-frame launches (untimed for `value`; the reference draws one frame
+    # per loop iteration, src/main.cpp:318-319, camera re-uploaded each time,
+    # :429): one frame alone (B = 1, F = 1: the interactive latency) and
+    # single-frame launches with 4 in flight (B = 1, F = 4).
+    single = None
+    if world == 1 and args.single_frame == "on":
+        single = single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, args.single_split,
+                               args.no_cull, render, warm, restore=split)
+
     # the reference's loop: one un-culled frame against one culled frame, alone
     speedup_ref = None
     if args.reference_loop == "on" and not args.no_cull and rank == 0:
@@ -563,6 +578,7 @@ def main():
                 "split_tiles": args.split,
                 "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "frame_latency_ms": round(latency_ms, 4),
+                "single_frame": single,
                 "culling": not args.no_cull,
                 "world_size": world,
                 "ranks": ranks,
@@ -579,6 +595,75 @@ def main():
         c[0].close()
     if rp["pricer"] is not None:
         rp["pricer"].close()
+
+
+def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_arg, no_cull, render, first,
+                  restore=(0, 16, 1), frames=20, alone_reps=9, inflight=4):
+    """Single-frame launches (sr_render_blocks of the whole frame): `alone` =
+    one frame at a time, each waited for (median of alone_reps; HIP events on
+    the context's stream), `inflight` = `frames` frames in launches of one,
+    `inflight` contexts and streams round robin, no host wait between them
+    (wall clock around the sequence, synchronised on both sides). Both on
+    contexts that have learned the frame's launch order. split_arg: split
+    tiles (sr_set_split) on these contexts for the measurement."""
+    import statistics
+
+    import torch
+
+    split = [int(x) for x in split_arg.split(":")] + [16, 1][len(split_arg.split(":")) - 1:]
+    pool = [(c[0], c[1], c[3]) for c in ctxs[:inflight]]
+    extra = []
+    while len(pool) < inflight:
+        rk = pkg.Renderer(dev.index)
+        rk.set_scene(scene)
+        rk.set_background(skybox)
+        rk.set_texture_array(arr)
+        rk.set_culling(not no_cull)
+        extra.append(rk)
+        pool.append((rk, torch.zeros((1,) + tuple(ctxs[0][1].shape[1:]), dtype=torch.uint8, device=dev),
+                     torch.cuda.Stream(dev)))
+    for rk, _, _ in pool:
+        rk.set_split(split[0], split[1], split[2])
+    n_cam = len(cams)
+    # each context learns the single-frame launch order (and split tiles) first
+    for k, (rk, tile_k, s_k) in enumerate(pool):
+        with torch.cuda.stream(s_k):
+            for j in range(2):
+                render(rk, (first + k + j) % n_cam, 1, tile_k, s_k)
+    for _, _, s_k in pool:
+        s_k.synchronize()
+    rk, tile_k, s_k = pool[0]
+    times = []
+    for j in range(alone_reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s_k):
+            e0.record(s_k)
+            render(rk, (first + j) % n_cam, 1, tile_k, s_k)
+            e1.record(s_k)
+        s_k.synchronize()
+        times.append(e0.elapsed_time(e1))
+    alone = statistics.median(times)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(frames):
+        rk, tile_k, s_k = pool[j % inflight]
+        with torch.cuda.stream(s_k):
+            render(rk, (first + j) % n_cam, 1, tile_k, s_k)
+    for _, _, s_k in pool:
+        s_k.synchronize()
+    torch.cuda.synchronize(dev)
+    per = (time.perf_counter() - t0) * 1e3 / frames
+    for rk, _, _ in pool:
+        rk.set_split(*restore)
+    for rk in extra:
+        rk.close()
+    return {
+        "alone": {"frames_per_launch": 1, "launches_in_flight": 1, "ms_per_frame": round(alone, 4),
+                  "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events"},
+        "inflight": {"frames_per_launch": 1, "launches_in_flight": inflight, "ms_per_frame": round(per, 4),
+                     "mpix_s": round(W * H / per / 1e3, 3), "frames": frames, "stat": "wall clock"},
+        "split_tiles": split_arg,
+    }
 
 
 FRAME_HASHES = ROOT / "tests" / "golden" / "frame_hashes.npz"
@@ -755,17 +840,25 @@ CPU_SWEEPS = (("640x360/1000", 640, 360, 1000), ("1920x1080/2000", 1920, 1080, 2
               ("3840x2160/4000", 3840, 2160, 4000))
 
 
-def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
+def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5, sweeps=CPU_SWEEPS, rays=PRESSR_RAYS):
     """The reference's press-R CPU geodesic (src/main.cpp:73-124, double
     temporaries, a std::vector per ray) on this host (BASELINE.md §3), the
     oracle's restatement of it ("port"; the reference app needs glm and GLFW,
     absent here):
-      - value: swept over a bounded sample of this frame's rows (every pixel's
-        camera ray, N steps), all threads of host_cpu(), -O2, median of 3;
-      - O0: the same at -O0 (the reference's CMake default build);
+      - value: swept over every row of this frame (every pixel's camera
+        ray, N steps; BASELINE.md §3 "wall time over the full frame"), all
+        threads of host_cpu(), -O2, median of 3 (sample_rows > 0: that many
+        rows around the centre instead, labelled as a sample);
+      - O0: the same at -O0 (the reference's CMake default build), on a
+        quarter of those rows (a sample, labelled);
       - configs: config 1 (one ray at N = 2000, microseconds per ray on one
         thread) and the 640x360 / 1000, 1920x1080 / 2000 and 3840x2160 / 4000
-        sweeps, each on a bounded row sample around the frame centre."""
+        sweeps: the full frame where it fits the time budget, else a row
+        sample around the frame centre (labelled);
+      - like_for_like: the reference shader itself (with scene intersection
+        and shading) on SwiftShader in the survey container, BASELINE.md §2,
+        quoted as context (it is not run here: the shader lives in the
+        reference, which does not travel to the GPU box)."""
     import statistics
 
     import numpy as np
@@ -794,8 +887,9 @@ def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
         return (y1 - y0) * w / dt / 1e6, y0, y1, pts, dt
 
     if sample_rows <= 0:
-        sample_rows = rows_for(W, H, N, budget_s)
+        sample_rows = H  # the full frame
     v2, y0, y1, pts, dt = rate(oracle.pressr_sweep, W, H, N, sample_rows)
+    full = (y0, y1) == (0, H)
     o0 = None
     if hasattr(oracle, "pressr_sweep_O0"):
         try:
@@ -804,7 +898,7 @@ def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
         except (FileNotFoundError, OSError):
             o0 = None
     configs = {}
-    for pos, fwd in PRESSR_RAYS:  # config 1: microseconds per ray, one thread
+    for pos, fwd in rays:  # config 1: microseconds per ray, one thread
         v = np.array(fwd, dtype=np.float32)
         v = (v * np.float32(1.0 / np.sqrt(np.float32(np.dot(v, v))))).tolist()
         n_pts = oracle.pressr_ray_repeat(pos, v, 2000, 2, 1)
@@ -818,20 +912,23 @@ def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
             reps *= 4
         configs[f"config1 dir {fwd}"] = {"value": round(el / reps * 1e6, 3), "unit": "us/ray", "cores": 1,
                                          "points": n_pts, "sample": f"{reps} traces, N = 2000, pos {pos}"}
-    for name, w, h, n in CPU_SWEEPS:
+    for name, w, h, n in sweeps:
         if (w, h, n) == (W, H, N):
             configs[name] = {"value": round(v2, 4), "unit": "Mpixels/s", "cores": threads, "same_as": "value"}
             continue
-        rv, a, b, p_, d = rate(oracle.pressr_sweep, w, h, n, rows_for(w, h, n, budget_s / 2))
+        rv, a, b, p_, d = rate(oracle.pressr_sweep, w, h, n, rows_for(w, h, n, budget_s))
         configs[name] = {"value": round(rv, 4), "unit": "Mpixels/s", "cores": threads,
-                         "sample": f"rows [{a},{b}) x {w} px, {p_} points, median of 3 runs {d:.2f} s"}
+                         "sample": ("full frame" if (a, b) == (0, h) else f"sample: rows [{a},{b}) of {h}")
+                         + f" x {w} px, {p_} points, median of 3 runs {d:.2f} s"}
     return {
         "value": round(v2, 4),
         "unit": "Mpixels/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"press-R loop (src/main.cpp:73-124) over rows [{y0},{y1}) x {W} px of the {W}x{H} frame, "
-                  f"{N} steps, {pts} points, median of 3 runs {dt:.2f} s, -O2, {threads} threads",
+        "sample": (f"full frame: press-R loop (src/main.cpp:73-124) over all {H} rows x {W} px of the {W}x{H} frame, "
+                   if full else
+                   f"sample: press-R loop (src/main.cpp:73-124) over rows [{y0},{y1}) x {W} px of the {W}x{H} frame, ")
+                  + f"{N} steps, {pts} points, median of 3 runs {dt:.2f} s, -O2, {threads} threads",
         "cores_basis": (f"sched_getaffinity allows {hc['affinity']} CPUs"
                         + (f", the cgroup quota {hc['cgroup_cpus']}" if hc["cgroup_cpus"] else ", no cgroup quota")
                         + f"; nproc {hc['nproc']}"),
@@ -840,6 +937,11 @@ def cpu_baseline(cam, W, H, N, sample_rows, budget_s=2.5):
         "O0": o0,
         "configs": configs,
         "note": "integrator only: the press-R loop does no scene intersection or shading (BASELINE.md §3)",
+        "like_for_like": {"value": 0.00225, "unit": "Mpixels/s", "cores": 8,
+                          "what": "the reference shader (assets/shaders/black_hole.frag, with intersection and "
+                                  "shading) on SwiftShader 4.1, 1920x1080 / 2000 steps, 922 s per frame",
+                          "where": "survey container, 8-core Xeon (BASELINE.md §2, SURVEY App. A); quoted as "
+                                   "context, not run on this host"},
     }
 
 

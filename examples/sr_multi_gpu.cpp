@@ -6,9 +6,19 @@
 //   per node    sr_wave_costs (one frame, root GPU) -> sr_block_costs ->
 //               sr_balanced_blocks: equal-length lists of 8-row blocks of
 //               about equal cost, one per rank
-//   per launch  every GPU: sr_render_block_list (B frames, its list) on its
-//               stream; ncclGather of the equal-size tiles to the root;
-//               root: sr_assemble_blocks (device kernel) -> B frames
+//   per launch  every GPU: sr_render_block_list (B frames, its list) on one
+//               of F slots (context + stream + tile), F launches in flight;
+//               ncclGather of the equal-size tiles to the root on the GPU's
+//               collective stream once that render is done; root:
+//               sr_assemble_blocks (device kernel) -> B frames. A slot's next
+//               render waits for the gather that read its tile (events only:
+//               the host never waits inside the timed loop)
+//
+// The pipeline is bench.py's (B = 8 frames per launch, F = 3 launches in
+// flight at N = 1): a frame's time is the latency of its longest rays'
+// waves (the photon ring), and launches in flight fill the SIMDs those waves
+// leave idle. At N = 1 there is nothing to gather: a slot's
+// tile is the frame (identity block list).
 //
 // Two ways to run it:
 //   one process, N GPUs     ./sr_multi_gpu --gpus N ...        (ncclCommInitAll)
@@ -64,15 +74,17 @@ namespace {
 constexpr int kBlockRows = 8;  // one 8x8 wave tile tall
 
 struct Args {
-    int gpus = 1, width = 1920, height = 1080, max_steps = 2000, frames = 16, batch = 8, warmup = 8;
+    int gpus = 1, width = 1920, height = 1080, max_steps = 2000, frames = 20, batch = 8, warmup = 24, inflight = 3;
     bool flyby = false;
+    bool force_gather = false;  // N = 1 too: price, gather (one rank) and reassemble (tests that path)
     std::string skybox, array, out_raw, id_file;
 };
 
 void usage() {
     std::printf(
         "sr_multi_gpu [--gpus N] [--width W] [--height H] [--max-steps N] [--frames K] [--batch B]\n"
-        "             [--warmup W] [--flyby] [--skybox PATH:W:H] [--array PATH:W:H:L] [--out-raw PATH]\n"
+        "             [--inflight F] [--warmup W] [--flyby] [--skybox PATH:W:H] [--array PATH:W:H:L]\n"
+        "             [--out-raw PATH] [--force-gather]\n"
         "             [--id-file PATH]   (one process per GPU: RANK / WORLD_SIZE / LOCAL_RANK from the env)\n");
 }
 
@@ -97,7 +109,9 @@ Args parse(int argc, char** argv) {
         else if (k == "--frames") a.frames = std::atoi(next());
         else if (k == "--batch") a.batch = std::atoi(next());
         else if (k == "--warmup") a.warmup = std::atoi(next());
+        else if (k == "--inflight") a.inflight = std::atoi(next());
         else if (k == "--flyby") a.flyby = true;
+        else if (k == "--force-gather") a.force_gather = true;
         else if (k == "--skybox") a.skybox = next();
         else if (k == "--array") a.array = next();
         else if (k == "--out-raw") a.out_raw = next();
@@ -131,31 +145,42 @@ std::vector<uint8_t> read_file(const std::string& path, size_t bytes) {
     return v;
 }
 
-// One GPU's share of the node.
-struct Device {
-    int dev = 0;
+// One launch slot of a GPU: its own context (pixel state, launch order), stream and tile.
+struct Slot {
     sr_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
-    uint8_t* tile = nullptr;     // B frames of per * kBlockRows rows
-    ncclComm_t comm = nullptr;
-    hipEvent_t r0 = nullptr, r1 = nullptr, g1 = nullptr;  // render start / end, gather end (timed launches)
-    double render_ms = 0.0, gather_ms = 0.0;
+    uint8_t* tile = nullptr;      // B frames of per * kBlockRows rows
+    uint8_t* stacked = nullptr;   // root, N > 1: the gathered tiles of every rank
+    uint8_t* frames = nullptr;    // root, N > 1: the reassembled frames (N = 1: the tile itself)
+    hipEvent_t rendered = nullptr;  // the slot's render is done (the collective stream waits for it)
+    hipEvent_t released = nullptr;  // the gather that read the tile is done (the slot's next render waits)
 };
 
-void setup_device(Device& d, const Args& a, const sr_scene& scene, size_t tile_bytes) {
-    CHECK_HIP(hipSetDevice(d.dev));
-    CHECK_SR(sr_create(&d.ctx, d.dev));
-    CHECK_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    CHECK_HIP(hipMalloc(&d.tile, tile_bytes));
-    CHECK_HIP(hipEventCreate(&d.r0));
-    CHECK_HIP(hipEventCreate(&d.r1));
-    CHECK_HIP(hipEventCreate(&d.g1));
-    CHECK_SR(sr_set_scene(d.ctx, &scene));
+// One GPU's share of the node: F slots and the stream of its collectives.
+struct Device {
+    int dev = 0;
+    ncclComm_t comm = nullptr;
+    hipStream_t cstream = nullptr;  // gathers and reassembly, in launch order (one communicator)
+    std::vector<Slot> slots;
+    // timed launches: render start / end on the slot's stream, gather (+ reassembly) end
+    std::vector<hipEvent_t> r0, r1, g1;
+    double render_ms_sum = 0.0, gather_ms_sum = 0.0;
+};
+
+void setup_slot(Slot& s, int dev, const Args& a, const sr_scene& scene, size_t tile_bytes) {
+    CHECK_HIP(hipSetDevice(dev));
+    CHECK_SR(sr_create(&s.ctx, dev));
+    CHECK_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    CHECK_HIP(hipMalloc(&s.tile, tile_bytes));
+    CHECK_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
+    CHECK_HIP(hipEventCreateWithFlags(&s.released, hipEventDisableTiming));
+    sr_ctx* ctx = s.ctx;
+    CHECK_SR(sr_set_scene(ctx, &scene));
     if (!a.skybox.empty()) {
         const auto f = split(a.skybox);
         const int w = std::atoi(f.at(1).c_str()), h = std::atoi(f.at(2).c_str());
         const auto px = read_file(f[0], (size_t)w * h * 3);
-        CHECK_SR(sr_set_background(d.ctx, px.data(), w, h, 3));
+        CHECK_SR(sr_set_background(ctx, px.data(), w, h, 3));
     } else {  // procedural stand-in: an 8x8-cell checker, 2048x1024 RGB
         const int w = 2048, h = 1024;
         std::vector<uint8_t> px((size_t)w * h * 3);
@@ -167,13 +192,13 @@ void setup_device(Device& d, const Args& a, const sr_scene& scene, size_t tile_b
                 p[1] = (uint8_t)(x * 255 / w);
                 p[2] = (uint8_t)(y * 255 / h);
             }
-        CHECK_SR(sr_set_background(d.ctx, px.data(), w, h, 3));
+        CHECK_SR(sr_set_background(ctx, px.data(), w, h, 3));
     }
     if (!a.array.empty()) {
         const auto f = split(a.array);
         const int w = std::atoi(f.at(1).c_str()), h = std::atoi(f.at(2).c_str()), l = std::atoi(f.at(3).c_str());
         const auto px = read_file(f[0], (size_t)w * h * l * 4);
-        CHECK_SR(sr_set_texture_array(d.ctx, px.data(), w, h, l, 4));
+        CHECK_SR(sr_set_texture_array(ctx, px.data(), w, h, l, 4));
     } else {  // opaque stand-in layers of the reference array's size (1601x1201, two layers)
         const int w = 1601, h = 1201, l = 2;
         std::vector<uint8_t> px((size_t)w * h * l * 4);
@@ -183,7 +208,7 @@ void setup_device(Device& d, const Args& a, const sr_scene& scene, size_t tile_b
             px[4 * i + 2] = (uint8_t)(i * 29);
             px[4 * i + 3] = 255;
         }
-        CHECK_SR(sr_set_texture_array(d.ctx, px.data(), w, h, l, 4));
+        CHECK_SR(sr_set_texture_array(ctx, px.data(), w, h, l, 4));
     }
 }
 
@@ -202,11 +227,12 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "--gpus %d: %d device(s) visible\n", world, ndev);
         return 1;
     }
-    if (a.batch < 1 || a.batch > 32 || a.frames < 1) {
-        std::fprintf(stderr, "--batch must be 1..32, --frames >= 1\n");
+    if (a.batch < 1 || a.batch > 32 || a.frames < 1 || a.inflight < 1 || a.inflight > 8 || a.warmup < 0) {
+        std::fprintf(stderr, "--batch must be 1..32, --inflight 1..8, --frames >= 1, --warmup >= 0\n");
         return 1;
     }
-    const int W = a.width, H = a.height, B = a.batch;
+    const int W = a.width, H = a.height, B = a.batch, F = a.inflight;
+    const bool gather = world > 1 || a.force_gather;  // N = 1: the tile is the frame
     const int nb = (H + kBlockRows - 1) / kBlockRows, nc = (W + 7) / 8;
     const int per = (nb + world - 1) / world;
     const size_t row_bytes = (size_t)W * 4, tile_frame = (size_t)per * kBlockRows * row_bytes;
@@ -224,7 +250,8 @@ int main(int argc, char** argv) {
     params.max_steps = a.max_steps;
     params.percent_black = -1.0f;  // the benchmark's setting
 
-    // ---- devices and communicators ----
+    // ---- devices and communicators (one per GPU: the gathers run in launch
+    // order on each GPU's collective stream) ----
     std::vector<Device> devs(per_process ? 1 : world);
     if (per_process) {
         devs[0].dev = local % ndev;
@@ -255,8 +282,14 @@ int main(int argc, char** argv) {
         CHECK_NCCL(ncclCommInitAll(comms.data(), world, ids.data()));
         for (int d = 0; d < world; d++) devs[d].comm = comms[d];
     }
-    for (auto& d : devs) setup_device(d, a, scene, tile_bytes);
     const bool root = rank == 0;  // devs[0] is the root GPU in the one-process mode
+    for (size_t k = 0; k < devs.size(); k++) {
+        Device& d = devs[k];
+        d.slots.resize(F);
+        for (auto& s : d.slots) setup_slot(s, d.dev, a, scene, tile_bytes);
+        CHECK_HIP(hipSetDevice(d.dev));
+        CHECK_HIP(hipStreamCreateWithFlags(&d.cstream, hipStreamNonBlocking));
+    }
     Device& r0 = devs[0];
 
     // cameras: the app's default, or its H-key flyby (src/main.cpp:404-410)
@@ -267,18 +300,21 @@ int main(int argc, char** argv) {
         if (a.flyby) CHECK_SR(sr_camera_hyperbolic_trajectory(&cams[f], 30.0f, 10.0f, (f + 0.5f) / n_total));
     }
 
-    // ---- pricing on the root GPU, lists to every rank ----
+    // ---- pricing on the root GPU, lists to every rank (N = 1: every block in order) ----
     std::vector<int> lists((size_t)world * per, -1);
     double max_over_mean = 1.0;
-    {
+    if (!gather) {
+        for (int b = 0; b < nb; b++) lists[b] = b;
+    } else {
         int32_t* d_costs = nullptr;
+        Slot& p0 = r0.slots[0];
         if (root) {
             CHECK_HIP(hipSetDevice(r0.dev));
             CHECK_HIP(hipMalloc(&d_costs, (size_t)nb * nc * 2 * sizeof(int32_t)));
-            CHECK_SR(sr_wave_costs(r0.ctx, &cams[0], &params, W, H, d_costs, r0.stream));
+            CHECK_SR(sr_wave_costs(p0.ctx, &cams[0], &params, W, H, d_costs, p0.stream));
             std::vector<int32_t> wc((size_t)nb * nc * 2);
-            CHECK_HIP(hipMemcpyAsync(wc.data(), d_costs, wc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, r0.stream));
-            CHECK_HIP(hipStreamSynchronize(r0.stream));
+            CHECK_HIP(hipMemcpyAsync(wc.data(), d_costs, wc.size() * sizeof(int32_t), hipMemcpyDeviceToHost, p0.stream));
+            CHECK_HIP(hipStreamSynchronize(p0.stream));
             CHECK_HIP(hipFree(d_costs));
             std::vector<double> cost(nb);
             CHECK_SR(sr_block_costs(wc.data(), nb, nc, 8.0, cost.data()));
@@ -298,112 +334,163 @@ int main(int argc, char** argv) {
             int* d_l = nullptr;
             CHECK_HIP(hipSetDevice(r0.dev));
             CHECK_HIP(hipMalloc(&d_l, lists.size() * sizeof(int)));
-            CHECK_HIP(hipMemcpyAsync(d_l, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, r0.stream));
-            CHECK_NCCL(ncclBroadcast(d_l, d_l, lists.size(), ncclInt32, 0, r0.comm, r0.stream));
-            CHECK_HIP(hipMemcpyAsync(lists.data(), d_l, lists.size() * sizeof(int), hipMemcpyDeviceToHost, r0.stream));
-            CHECK_HIP(hipStreamSynchronize(r0.stream));
+            CHECK_HIP(hipMemcpyAsync(d_l, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice, r0.cstream));
+            CHECK_NCCL(ncclBroadcast(d_l, d_l, lists.size(), ncclInt32, 0, r0.comm, r0.cstream));
+            CHECK_HIP(hipMemcpyAsync(lists.data(), d_l, lists.size() * sizeof(int), hipMemcpyDeviceToHost, r0.cstream));
+            CHECK_HIP(hipStreamSynchronize(r0.cstream));
             CHECK_HIP(hipFree(d_l));
         }
     }
 
-    // root buffers: the gathered tiles, the lists on the device, the frames
-    uint8_t *stacked = nullptr, *frames = nullptr;
+    // root buffers (gather): per slot the gathered tiles and the frames; the lists on the device
     int* d_lists = nullptr;
-    if (root) {
+    if (root && gather) {
         CHECK_HIP(hipSetDevice(r0.dev));
-        CHECK_HIP(hipMalloc(&stacked, tile_bytes * world));
-        CHECK_HIP(hipMalloc(&frames, (size_t)B * H * row_bytes));
+        for (auto& s : r0.slots) {
+            CHECK_HIP(hipMalloc(&s.stacked, tile_bytes * world));
+            CHECK_HIP(hipMalloc(&s.frames, (size_t)B * H * row_bytes));
+        }
         CHECK_HIP(hipMalloc(&d_lists, lists.size() * sizeof(int)));
         CHECK_HIP(hipMemcpy(d_lists, lists.data(), lists.size() * sizeof(int), hipMemcpyHostToDevice));
     }
 
-    // one launch: frames [first, first + n) on every GPU, gathered, reassembled
-    auto launch = [&](int first, int n, bool timed) {
-        for (size_t k = 0; k < devs.size(); k++) {
-            Device& d = devs[k];
-            const int r = per_process ? rank : (int)k;
+    // launch j: frames [first, first + n) on slot j % F of every GPU, then
+    // (N > 1) the gather and the reassembly on the collective streams. Events
+    // order it: no host wait. t >= 0: the timed launch's index.
+    int launches = 0;
+    auto launch = [&](int first, int n, int t) {
+        const int k = launches % F;
+        const bool reuse = launches >= F;
+        launches++;
+        for (size_t i = 0; i < devs.size(); i++) {
+            Device& d = devs[i];
+            Slot& s = d.slots[k];
+            const int r = per_process ? rank : (int)i;
             CHECK_HIP(hipSetDevice(d.dev));
-            if (timed) CHECK_HIP(hipEventRecord(d.r0, d.stream));
-            CHECK_SR(sr_render_block_list(d.ctx, &cams[first], n, &params, W, H, kBlockRows, &lists[(size_t)r * per],
-                                          per, d.tile, row_bytes, tile_frame, d.stream));
-            if (timed) CHECK_HIP(hipEventRecord(d.r1, d.stream));
-        }
-        // equal-size tiles to the root over xGMI (each peer on its own link)
-        CHECK_NCCL(ncclGroupStart());
-        for (size_t k = 0; k < devs.size(); k++) {
-            Device& d = devs[k];
-            const bool is_root = per_process ? root : k == 0;
-            CHECK_NCCL(ncclGather(d.tile, is_root ? stacked : nullptr, tile_bytes, ncclUint8, 0, d.comm, d.stream));
-        }
-        CHECK_NCCL(ncclGroupEnd());
-        for (auto& d : devs)
-            if (timed) {
-                CHECK_HIP(hipSetDevice(d.dev));
-                CHECK_HIP(hipEventRecord(d.g1, d.stream));
+            if (reuse && gather) CHECK_HIP(hipStreamWaitEvent(s.stream, s.released, 0));  // its tile was gathered
+            if (t >= 0) CHECK_HIP(hipEventRecord(d.r0[t], s.stream));
+            CHECK_SR(sr_render_block_list(s.ctx, &cams[first], n, &params, W, H, kBlockRows, &lists[(size_t)r * per],
+                                          per, s.tile, row_bytes, tile_frame, s.stream));
+            if (t >= 0) CHECK_HIP(hipEventRecord(d.r1[t], s.stream));
+            if (gather) {
+                CHECK_HIP(hipEventRecord(s.rendered, s.stream));
+                CHECK_HIP(hipStreamWaitEvent(d.cstream, s.rendered, 0));
             }
-        if (root) {
-            CHECK_HIP(hipSetDevice(r0.dev));
-            CHECK_SR(sr_assemble_blocks(stacked, tile_bytes, tile_frame, d_lists, world, per, H, kBlockRows, row_bytes,
-                                        frames, (size_t)H * row_bytes, n, 1, r0.stream));
         }
-        if (timed) {  // per-launch device times (the launches of a run are sequential per GPU)
+        if (gather) {
+            // equal-size tiles to the root over xGMI (each peer on its own link)
+            CHECK_NCCL(ncclGroupStart());
+            for (size_t i = 0; i < devs.size(); i++) {
+                Device& d = devs[i];
+                Slot& s = d.slots[k];
+                const bool is_root = per_process ? root : i == 0;
+                CHECK_NCCL(ncclGather(s.tile, is_root ? r0.slots[k].stacked : nullptr, tile_bytes, ncclUint8, 0, d.comm,
+                                      d.cstream));
+            }
+            CHECK_NCCL(ncclGroupEnd());
+            if (root) {
+                Slot& s = r0.slots[k];
+                CHECK_HIP(hipSetDevice(r0.dev));
+                CHECK_SR(sr_assemble_blocks(s.stacked, tile_bytes, tile_frame, d_lists, world, per, H, kBlockRows,
+                                            row_bytes, s.frames, (size_t)H * row_bytes, n, 1, r0.cstream));
+            }
             for (auto& d : devs) {
-                CHECK_HIP(hipEventSynchronize(d.g1));
-                float rm = 0.f, gm = 0.f;
-                CHECK_HIP(hipEventElapsedTime(&rm, d.r0, d.r1));
-                CHECK_HIP(hipEventElapsedTime(&gm, d.r1, d.g1));
-                d.render_ms += rm;
-                d.gather_ms += gm;
+                CHECK_HIP(hipSetDevice(d.dev));
+                CHECK_HIP(hipEventRecord(d.slots[k].released, d.cstream));
+                if (t >= 0) CHECK_HIP(hipEventRecord(d.g1[t], d.cstream));
             }
+        } else if (t >= 0) {
+            CHECK_HIP(hipEventRecord(r0.g1[t], r0.slots[k].stream));
         }
+        return k;
     };
     auto sync_all = [&]() {
         for (auto& d : devs) {
             CHECK_HIP(hipSetDevice(d.dev));
-            CHECK_HIP(hipStreamSynchronize(d.stream));
+            for (auto& s : d.slots) CHECK_HIP(hipStreamSynchronize(s.stream));
+            CHECK_HIP(hipStreamSynchronize(d.cstream));
         }
     };
-    for (int f = 0; f < a.warmup; f += B) launch(f, std::min(B, a.warmup - f), false);
+    const int n_timed = (a.frames + B - 1) / B;
+    for (auto& d : devs) {
+        CHECK_HIP(hipSetDevice(d.dev));
+        for (auto* v : {&d.r0, &d.r1, &d.g1}) {
+            v->resize(n_timed);
+            for (auto& e : *v) CHECK_HIP(hipEventCreate(&e));
+        }
+    }
+    // warmup: every slot's context learns the launch order of its tiles
+    for (int f = 0; f < a.warmup; f += B) launch(f, std::min(B, a.warmup - f), -1);
     sync_all();
     const auto t0 = std::chrono::steady_clock::now();
-    int last_n = 0;
-    for (int f = 0; f < a.frames; f += B) {
+    int last_n = 0, last_k = 0, t = 0;
+    for (int f = 0; f < a.frames; f += B, t++) {
         last_n = std::min(B, a.frames - f);
-        launch(a.warmup + f, last_n, true);
+        last_k = launch(a.warmup + f, last_n, t);
     }
     sync_all();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // device times of the timed launches (read after the loop): the launches
+    // overlap, so render_ms sums to more than the wall time
+    for (auto& d : devs) {
+        double rm = 0.0, gm = 0.0;
+        for (int i = 0; i < n_timed; i++) {
+            float x = 0.f, y = 0.f;
+            CHECK_HIP(hipEventElapsedTime(&x, d.r0[i], d.r1[i]));
+            CHECK_HIP(hipEventElapsedTime(&y, d.r1[i], d.g1[i]));
+            rm += x;
+            gm += y;
+        }
+        d.render_ms_sum = rm;
+        d.gather_ms_sum = gm;
+    }
 
     if (root && !a.out_raw.empty()) {  // the run's last frame
         std::vector<uint8_t> h((size_t)H * row_bytes);
+        const Slot& s = r0.slots[last_k];
+        const uint8_t* src = gather ? s.frames + (size_t)(last_n - 1) * H * row_bytes
+                                       : s.tile + (size_t)(last_n - 1) * tile_frame;
         CHECK_HIP(hipSetDevice(r0.dev));
-        CHECK_HIP(hipMemcpy(h.data(), frames + (size_t)(last_n - 1) * H * row_bytes, h.size(), hipMemcpyDeviceToHost));
+        CHECK_HIP(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost));
         std::ofstream(a.out_raw, std::ios::binary).write(reinterpret_cast<const char*>(h.data()), (std::streamsize)h.size());
     }
     if (root) {
         std::printf("{\"tool\": \"sr_multi_gpu\", \"mode\": \"%s\", \"world_size\": %d, \"width\": %d, \"height\": %d, "
-                    "\"max_steps\": %d, \"frames\": %d, \"frames_per_launch\": %d, \"camera\": \"%s\", "
+                    "\"max_steps\": %d, \"frames\": %d, \"warmup\": %d, \"frames_per_launch\": %d, "
+                    "\"launches_in_flight\": %d, \"camera\": \"%s\", "
                     "\"value\": %.3f, \"unit\": \"Mpixels/s\", \"ms_per_frame\": %.4f, \"balance_max_over_mean\": %.4f, "
-                    "\"collective\": \"ncclGather of equal-size tiles\", \"ranks\": [",
+                    "\"timing\": \"wall clock around the timed launches, streams synchronised on both sides\", "
+                    "\"collective\": \"%s\", \"ranks\": [",
                     per_process ? "process per GPU (ncclCommInitRank)" : "one process (ncclCommInitAll)", world, W, H,
-                    a.max_steps, a.frames, B, a.flyby ? "flyby" : "static", (double)W * H * a.frames / sec / 1e6,
-                    sec * 1e3 / a.frames, max_over_mean);
+                    a.max_steps, a.frames, a.warmup, B, F, a.flyby ? "flyby" : "static",
+                    (double)W * H * a.frames / sec / 1e6, sec * 1e3 / a.frames, max_over_mean,
+                    gather ? "ncclGather of equal-size tiles on each GPU's collective stream"
+                              : "none (one GPU: the tile is the frame)");
         for (size_t k = 0; k < devs.size(); k++)
-            std::printf("%s{\"device\": %d, \"render_ms_per_frame\": %.4f, \"gather_ms_per_frame\": %.4f}",
-                        k ? ", " : "", devs[k].dev, devs[k].render_ms / a.frames, devs[k].gather_ms / a.frames);
+            std::printf("%s{\"device\": %d, \"render_ms_per_launch\": %.4f, \"render_ms_per_frame\": %.4f, "
+                        "\"gather_ms_per_frame\": %.4f}",
+                        k ? ", " : "", devs[k].dev, devs[k].render_ms_sum / n_timed, devs[k].render_ms_sum / a.frames,
+                        devs[k].gather_ms_sum / a.frames);
         std::printf("]}\n");
     }
     for (auto& d : devs) {
         CHECK_HIP(hipSetDevice(d.dev));
-        sr_destroy(d.ctx);
-        (void)hipFree(d.tile);
-        (void)hipStreamDestroy(d.stream);
+        for (auto& s : d.slots) {
+            sr_destroy(s.ctx);
+            (void)hipFree(s.tile);
+            if (s.stacked) (void)hipFree(s.stacked);
+            if (s.frames) (void)hipFree(s.frames);
+            (void)hipStreamDestroy(s.stream);
+            (void)hipEventDestroy(s.rendered);
+            (void)hipEventDestroy(s.released);
+        }
+        for (auto* v : {&d.r0, &d.r1, &d.g1})
+            for (auto& e : *v) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(d.cstream);
         (void)ncclCommDestroy(d.comm);
     }
-    if (root) {
+    if (d_lists) {
         CHECK_HIP(hipSetDevice(r0.dev));
-        (void)hipFree(stacked);
-        (void)hipFree(frames);
         (void)hipFree(d_lists);
     }
     return 0;

@@ -51,6 +51,8 @@ extern "C" {
 #define SR_MAX_BOXES        3
 #define SR_MAX_OBJECTS      21
 #define SR_MAX_POINTS       1000
+/* max_steps limit: the integrate -> shade hand-off packs a ray's step count into 24 bits */
+#define SR_MAX_STEPS        ((1 << 24) - 1)
 
 /* Object type codes — black_hole.frag:162-171 == ObjectType (object.h:7-19) */
 #define SR_OBJECT_SPHERE      0
@@ -270,8 +272,8 @@ int sr_set_test_ray(sr_ctx* ctx, const sr_test_ray* test_ray);
  * is the bottom row) into dev_rgba8 (device memory, row r at
  * dev_rgba8 + (r - row_begin) * pitch_bytes). Asynchronous on `stream`.
  * A context reuses its per-frame scratch (pixel state, launch order), so its
- * renders must be ordered: one stream per context, or synchronise between
- * streams. */
+ * renders are ordered: a launch on another stream than the context's last
+ * one first waits (hipStreamWaitEvent) for the work of that stream. */
 int sr_render(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width,
               int height, int row_begin, int row_end, uint8_t* dev_rgba8,
               size_t pitch_bytes, sr_stream stream);
@@ -371,6 +373,15 @@ int sr_set_split(sr_ctx* ctx, int max_tiles, int lanes_per_wave, int min_steps);
 
 /* Rows a sr_render_blocks call with these arguments writes. */
 int sr_blocks_row_count(int height, int block_rows, int block_first, int block_step);
+
+/* Runtime invariant counters of a context (not in the reference), after its
+ * launched frames are done: out[0] = pixels the shade kernel found stopped at
+ * a hit classified opaque in the step loop whose shaded alpha was not 1 (the
+ * classification is exact where it claims, DESIGN.md §5, so this stays 0; a
+ * non-zero count means such rays were written without the rest of their
+ * path), out[1] = stream-ordered frees (hipFreeAsync) that failed (a leak).
+ * Writes min(n, 2) counters. */
+int sr_diag_counters(sr_ctx* ctx, int64_t* out, int n);
 
 /* sizeof of the ABI structs, for binding checks: sr_camera, sr_params,
  * sr_scene, sr_test_ray, sr_material, sr_light (in that order). */

@@ -194,6 +194,7 @@ SIGNATURES = {
     "sr_render_block_list": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, C.POINTER(_i), _i, _p,
                                   C.c_size_t, C.c_size_t, _p]),
     "sr_abi_struct_sizes": (_i, [C.POINTER(C.c_size_t), _i]),
+    "sr_diag_counters": (_i, [_p, C.POINTER(C.c_int64), _i]),
     "sr_test_ray_points": (_i, [C.POINTER(C.c_float), C.POINTER(C.c_float), _i, _i, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
     "sr_block_costs": (_i, [_p, _i, _i, C.c_double, _p]),
     "sr_balanced_blocks": (_i, [_p, _i, _i, _p, _i, C.POINTER(_i)]),

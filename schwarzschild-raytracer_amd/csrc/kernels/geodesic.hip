@@ -1576,7 +1576,11 @@ static_assert(PS_PLANES + 16 == SR_PS_FIELDS, "pixel-state layout");
 // key = slot * 8 + face in [-24, 167]: slots -3 .. SR_MAX_OBJECTS - 1
 #define PS_KEY_BIAS 24
 static_assert((SR_MAX_OBJECTS - 1) * 8 + 7 + PS_KEY_BIAS < 256, "hit key fits 8 bits");
-__device__ __forceinline__ int ps_word(int st, int nh, int steps) { return st | (nh << 3) | (steps << 8); }
+// steps <= SR_MAX_STEPS (sr_api.cpp build_frame): 24 bits
+static_assert(SR_MAX_STEPS < (1 << 24), "step count fits the packed word");
+__device__ __forceinline__ int ps_word(int st, int nh, int steps) {
+    return (int)((uint32_t)st | ((uint32_t)nh << 3) | ((uint32_t)steps << 8));
+}
 
 struct Ray {
     f3 ro, rd, nv, tv;
@@ -2259,7 +2263,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 // sector costs a read-modify-write)
                 float4* h = reinterpret_cast<float4*>(log.ps.hit(log.id(), log.n));
                 h[0] = make_float4(hit.p.x, hit.p.y, hit.p.z,
-                                   __int_as_float((hit.slot * 8 + hit.face + PS_KEY_BIAS) | (r.steps << 8)));
+                                   __int_as_float((int)((uint32_t)(hit.slot * 8 + hit.face + PS_KEY_BIAS) |
+                                                                  ((uint32_t)r.steps << 8))));
                 h[1] = make_float4(r.rd.x, r.rd.y, r.rd.z, 0.0f);
                 log.n++;
                 if (op == OP_OPAQUE) return ST_HIT;
@@ -2548,7 +2553,8 @@ __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __res
                                                       float* __restrict__ ps_base, size_t ps_n,
                                                       uint8_t* __restrict__ out, size_t pitch,
                                                       float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
-                                                      int* __restrict__ list, int* __restrict__ count) {
+                                                      int* __restrict__ list, int* __restrict__ count,
+                                                      int* __restrict__ diag) {
     const int vblock = blockIdx.y * gridDim.x + blockIdx.x;  // frame f's tiles are rows f*gy .. of the grid
     const int f = vblock / fr.tiles, block = vblock - f * fr.tiles;
     Pix q;
@@ -2596,6 +2602,11 @@ __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __res
             list[atomicAdd(count, 1)] = (int)id;
             return;
         }
+        // an ST_HIT pixel ends at an opaque-classified hit (hit_opacity, exact
+        // where it claims): its shaded alpha is 1. Counted if ever not
+        // (sr_diag_counters; the tests assert 0): such a ray has no
+        // resumable state and is written without the rest of its path.
+        if (st == ST_HIT) atomicAdd(diag, 1);
         if (st == ST_FLAT || st == ST_BG)  // ro only for the flat intersect
             finish_ray(sc, segs, fr, tx, st, st == ST_FLAT ? ps.get3(PS_RO, id) : F3(0.0f, 0.0f, 0.0f),
                        F3(rec.y, rec.z, rec.w), frag);
@@ -2662,7 +2673,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                                          const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
                                          const sr_dev_frame* fr, uint8_t* out, size_t pitch, float* dbg_rgba,
                                          int32_t* dbg_steps, float* ps, size_t ps_n, int* list, int* count,
-                                         int* order, int* cost, hipEvent_t* ev4, hipStream_t stream) {
+                                         int* order, int* cost, int* diag, hipEvent_t* ev4, hipStream_t stream) {
     dim3 block(256);
     dim3 grid((fr->width + 15) / 16, (fr->nrows + 15) / 16);
     if (grid.x == 0 || grid.y == 0) return hipSuccess;
@@ -2693,7 +2704,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                            tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
     hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
-                       out, pitch, dbg_rgba, dbg_steps, list, count);
+                       out, pitch, dbg_rgba, dbg_steps, list, count, diag);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
     unsigned nb = (nblocks * B < 1024u ? nblocks * B : 1024u) * SR_WG_PER_TILE;
     if (cull)

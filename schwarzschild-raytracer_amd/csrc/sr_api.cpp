@@ -24,7 +24,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                                          const sr_dev_frame* fr,
                                          uint8_t* out, size_t pitch, float* dbg_rgba, int32_t* dbg_steps,
                                          float* ps, size_t ps_n, int* list, int* count, int* order, int* cost,
-                                         hipEvent_t* ev4, hipStream_t stream);
+                                         int* diag, hipEvent_t* ev4, hipStream_t stream);
 
 namespace {
 
@@ -96,6 +96,14 @@ struct sr_ctx {
     // may still read the context's buffers, and for nothing else on the device
     hipStream_t last_stream = nullptr;
     bool launched = false;
+    // a launch on another stream than the last one first waits for it (this
+    // event, recorded on the old stream): the context's scratch and the
+    // stream-ordered frees on last_stream stay ordered after every launch
+    hipEvent_t order_ev = nullptr;
+    // stream-ordered frees whose hipFreeAsync failed (sr_diag_counters)
+    int64_t free_errors = 0;
+    // device counter of the shade kernel's invariant check (sr_diag_counters)
+    int* d_diag = nullptr;
     // optional per-kernel timing: 4 events per frame (before integrate, after
     // integrate, after shade, after resume), a ring of `timing_cap` frames
     std::vector<hipEvent_t> tev;
@@ -312,7 +320,7 @@ inline bool hip_ok(hipError_t e) { return e == hipSuccess; }
 // frames (its last launch stream; `s` before its first launch). hipFree would
 // synchronise the whole device.
 void release(sr_ctx* ctx, void* p, hipStream_t s) {
-    if (p) (void)hipFreeAsync(p, ctx->launched ? ctx->last_stream : s);
+    if (p && !hip_ok(hipFreeAsync(p, ctx->launched ? ctx->last_stream : s))) ctx->free_errors++;
 }
 
 // LRU eviction down to kCacheEntries - 1 entries (one is about to be added).
@@ -602,7 +610,8 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
     if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
     if (p->filter_mode != SR_FILTER_LERP && p->filter_mode != SR_FILTER_WEIGHTED) return SR_E_INVALID;
-    if (p->max_steps < 0 || p->max_steps > (1 << 24)) return SR_E_INVALID;
+    // the hand-off packs a ray's step count into 24 bits (geodesic.hip ps_word)
+    if (p->max_steps < 0 || p->max_steps > SR_MAX_STEPS) return SR_E_INVALID;
     std::memset(&fr, 0, sizeof fr);
     build_cam(cam, fr.cam[0]);
     fr.batch = 1;
@@ -653,7 +662,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.batch = n_frames;
     // the black hole's u window (geodesic.hip SR_BH_WINDOW): chord origins within r = 100
     fr.num_budget = ctx->h_scene.num_budget;
-    fr.win_ok = fr.uf_radius <= 100.5f;
+    fr.win_ok = fr.uf_radius <= 100.0f;
     for (int f = 0; f < n_frames; f++) {
         const float* q = fr.cam[f].pos;
         if (!((double)q[0] * q[0] + (double)q[1] * q[1] + (double)q[2] * q[2] <= 1.0e4)) fr.win_ok = 0;
@@ -671,6 +680,10 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.wave_cost = d_wave_cost;
     if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (ctx->launched && s != ctx->last_stream) {  // ordered after the launches on the previous stream
+        if (!hip_ok(hipEventRecord(ctx->order_ev, ctx->last_stream)) || !hip_ok(hipStreamWaitEvent(s, ctx->order_ev, 0)))
+            return SR_E_HIP;
+    }
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, s, &tbl);
     if (rc != SR_OK) return rc;
@@ -687,6 +700,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     }
     hipError_t e = sr_launch_geodesic(ctx->d_scene, tbl, ctx->d_segs, ctx->d_bg, ctx->d_arr, ctx->d_opq, &fr, out, pitch,
                                       dbg_rgba, dbg_steps, ctx->d_ps, ctx->ps_n, ctx->d_list, ctx->d_count, order, cost,
+                                      ctx->d_diag,
                                       ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
                                       s);
     ctx->last_stream = s;
@@ -754,12 +768,19 @@ int sr_create(sr_ctx** out, int hip_device) {
         sr_destroy(c);
         return SR_E_HIP;
     }
+    if (!hip_ok(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming))) {
+        c->order_ev = nullptr;
+        sr_destroy(c);
+        return SR_E_HIP;
+    }
     if (!hip_ok(hipMalloc(&c->d_scene, sizeof(sr_dev_scene))) ||
-        !hip_ok(hipMalloc(&c->d_segs, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float)))) {
+        !hip_ok(hipMalloc(&c->d_segs, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float))) ||
+        !hip_ok(hipMalloc(reinterpret_cast<void**>(&c->d_diag), sizeof(int)))) {
         sr_destroy(c);
         return SR_E_NOMEM;
     }
     if (!hip_ok(hipMemsetAsync(c->d_scene, 0, sizeof(sr_dev_scene), c->upload)) ||
+        !hip_ok(hipMemsetAsync(c->d_diag, 0, sizeof(int), c->upload)) ||
         !hip_ok(hipMemsetAsync(c->d_segs, 0, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float),
                                c->upload)) ||
         !hip_ok(hipStreamSynchronize(c->upload))) {
@@ -783,6 +804,7 @@ void sr_destroy(sr_ctx* c) {
     (void)wait_ctx(c);
     if (c->d_scene) (void)hipFree(c->d_scene);
     if (c->d_segs) (void)hipFree(c->d_segs);
+    if (c->d_diag) (void)hipFree(c->d_diag);
     // the rest came from the stream-ordered allocator: freed the same way,
     // then waited for (the context's frames are done: wait_ctx)
     const hipStream_t s = c->upload;
@@ -802,7 +824,20 @@ void sr_destroy(sr_ctx* c) {
         (void)hipStreamDestroy(s);
     }
     for (hipEvent_t e : c->tev) (void)hipEventDestroy(e);
+    if (c->order_ev) (void)hipEventDestroy(c->order_ev);
     delete c;
+}
+
+int sr_diag_counters(sr_ctx* c, int64_t* out, int n) {
+    if (!c || !out || n < 0) return SR_E_INVALID;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
+    int dropped = 0;
+    if (!hip_ok(hipMemcpyAsync(&dropped, c->d_diag, sizeof(int), hipMemcpyDeviceToHost, c->upload)) ||
+        !hip_ok(hipStreamSynchronize(c->upload)))
+        return SR_E_HIP;
+    const int64_t v[2] = {dropped, c->free_errors};
+    for (int i = 0; i < n && i < 2; i++) out[i] = v[i];
+    return SR_OK;
 }
 
 int sr_set_background(sr_ctx* c, const uint8_t* px, int w, int h, int ch) {

@@ -295,7 +295,11 @@ class ListSchedule:
 class FrameGather:
     """Preallocated gather of equal-size tiles to rank 0 (collective). A tile
     of [B, tile_rows, W, C] holds B frames (a batched launch); __call__(n)
-    gathers the first n of them and returns the [n, H, W, C] frames."""
+    gathers the first n of them and returns the [n, H, W, C] frames.
+
+    On device tiles with block lists the returned frames live in a buffer
+    this gather keeps and reuses: the next call overwrites them (clone to
+    keep one)."""
 
     def __init__(self, tile, world: int, rank: int, height: int, block_rows: int, group=None, lists=None):
         self.world, self.rank, self.height, self.block_rows, self.group = world, rank, height, block_rows, group
@@ -309,17 +313,20 @@ class FrameGather:
         if rank == 0 and world > 1:
             self.stacked = tile.new_empty((world,) + tuple(tile.shape))
             self.views = [self.stacked[i] for i in range(world)]
+        if lists is not None:
+            self.set_lists(lists)  # checks the lists cover the frame (list_sources)
 
     def set_lists(self, lists):
         """Switch to balanced_blocks lists; their block sources go to the tiles'
         device now, outside any launch."""
+        src = list_sources(lists, self.height, self.block_rows)  # asserts the lists cover the frame
         self.lists = lists
         self._src = None
         self._dev_lists = None
         if type(self.tile).__module__.startswith("torch"):
             import torch
 
-            self._src = torch.as_tensor(list_sources(lists, self.height, self.block_rows), device=self.tile.device)
+            self._src = torch.as_tensor(src, device=self.tile.device)
             if self.tile.device.type == "cuda":
                 self._dev_lists = torch.tensor([b for l in lists for b in l], dtype=torch.int32,
                                                device=self.tile.device)

@@ -65,6 +65,13 @@ class Renderer:
         k = min(n.value, max_frames)
         return np.frombuffer(buf, dtype=np.float32, count=3 * k).reshape(k, 3).copy()
 
+    def diag_counters(self) -> dict:
+        """sr_diag_counters after this context's frames: opaque-classified hits
+        whose shaded alpha was not 1 (must stay 0) and failed stream-ordered frees."""
+        buf = (C.c_int64 * 2)()
+        abi.check(self.lib.sr_diag_counters(self.ctx, buf, 2), "sr_diag_counters")
+        return {"hit_not_opaque": int(buf[0]), "free_errors": int(buf[1])}
+
     def last_order(self) -> np.ndarray:
         """The launch codes the last frame left for the next one (tile << 8, | 0x80 | sub when split, -1 unused)."""
         n = C.c_int()

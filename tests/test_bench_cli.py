@@ -68,3 +68,19 @@ def test_frames_per_launch_by_rank_share():
     assert bench.launches_in_flight(4) == 3 and bench.launches_in_flight(1) == 4
     a = _parse(["--batch", "2", "--split", "32:4:1000"])
     assert a.batch == 2 and a.split == "32:4:1000"
+
+
+def test_cpu_baseline_sweeps_the_full_frame():
+    """`value` is the wall time over the full frame (every
+    row), the like-for-like SwiftShader figure is quoted beside it."""
+    import bench
+    import srpkg
+
+    cam = srpkg.load_package().abi.default_camera()
+    out = bench.cpu_baseline(cam, 48, 27, 60, 0, sweeps=(("48x27/60", 48, 27, 60),), rays=())
+    assert out["sample"].startswith("full frame") and "all 27 rows" in out["sample"]
+    assert out["value"] > 0 and out["kind"] == "port" and out["cores"] >= 1
+    assert out["configs"]["48x27/60"]["same_as"] == "value"
+    assert out["like_for_like"]["value"] == 0.00225
+    part = bench.cpu_baseline(cam, 48, 27, 60, 9, sweeps=(), rays=())
+    assert part["sample"].startswith("sample: ") and "rows [9,18)" in part["sample"]

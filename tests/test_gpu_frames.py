@@ -190,10 +190,12 @@ def test_config5_still_8k(pkg, fh, assets):
 
 def test_cpp_multi_gpu_driver_frame(pkg, fh, assets, tmp_path):
     """examples/sr_multi_gpu (C++ over the C-ABI, RCCL): the node-level path -
-    sr_wave_costs -> sr_block_costs -> sr_balanced_blocks, sr_render_block_list
-    per GPU, ncclGather of the tiles (ncclCommInitAll over the box's one GPU),
-    sr_assemble_blocks - renders the headline frame with the reference's
-    textures (raw files) equal row for row to the oracle fixture."""
+    sr_render_block_list on F slots per GPU with B frames per launch and the
+    gathers on a collective stream, ordered by events (no host wait in the
+    timed loop); N > 1 adds sr_wave_costs -> sr_block_costs ->
+    sr_balanced_blocks and ncclGather + sr_assemble_blocks - renders the
+    headline frame with the reference's textures (raw files) equal row for
+    row to the oracle fixture, and reports its rate."""
     import json
     import subprocess
 
@@ -208,15 +210,26 @@ def test_cpp_multi_gpu_driver_frame(pkg, fh, assets, tmp_path):
         a = np.concatenate([a, np.full(a.shape[:-1] + (1,), 255, np.uint8)], axis=-1)
     (tmp_path / "arr.rgba").write_bytes(a.tobytes())
     out = tmp_path / "frame.rgba"
-    cmd = [str(exe), "--gpus", "1", "--width", str(W), "--height", str(H), "--max-steps", str(N), "--frames", "4",
-           "--batch", "2", "--warmup", "2", "--skybox", f"{tmp_path / 'sky.rgb'}:{sky.shape[1]}:{sky.shape[0]}",
+    cmd = [str(exe), "--gpus", "1", "--width", str(W), "--height", str(H), "--max-steps", str(N), "--frames", "7",
+           "--batch", "2", "--inflight", "3", "--warmup", "6",
+           "--skybox", f"{tmp_path / 'sky.rgb'}:{sky.shape[1]}:{sky.shape[0]}",
            "--array", f"{tmp_path / 'arr.rgba'}:{a.shape[2]}:{a.shape[1]}:{a.shape[0]}", "--out-raw", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["world_size"] == 1 and line["frames"] == 4 and line["ranks"][0]["render_ms_per_frame"] > 0
+    # the pipeline: 2 frames per launch, 3 launches in flight (the last launch renders one frame)
+    assert line["world_size"] == 1 and line["frames"] == 7 and line["ranks"][0]["render_ms_per_frame"] > 0
+    assert line["frames_per_launch"] == 2 and line["launches_in_flight"] == 3
+    assert line["unit"] == "Mpixels/s" and line["value"] > 0 and line["ms_per_frame"] > 0
     frame = np.frombuffer(out.read_bytes(), dtype=np.uint8).reshape(H, W, 4)
-    compare(pkg, fh, "c3", frame, None, "C++ RCCL driver")
+    compare(pkg, fh, "c3", frame, None, "C++ driver pipeline")
+    # the N > 1 path on the one GPU: priced lists, ncclGather (one rank) and sr_assemble_blocks
+    r = subprocess.run(cmd + ["--force-gather"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["collective"].startswith("ncclGather") and line["value"] > 0
+    frame = np.frombuffer(out.read_bytes(), dtype=np.uint8).reshape(H, W, 4)
+    compare(pkg, fh, "c3", frame, None, "C++ RCCL driver (gather path)")
 
 
 def test_frame_gather_device_reassembly(pkg, fh, assets):

@@ -605,3 +605,45 @@ def test_two_contexts_alternating_shapes_in_flight(pkg, textures):
                     assert np.array_equal(o[0, s_ * 8:s_ * 8 + n], full[b * 8:b * 8 + n]), (key, b)
     for c in ctxs:
         c.close()
+
+
+def test_one_context_alternating_streams(pkg, textures):
+    """A context's launches on another stream than its last one wait for that
+    stream first (sr_api.cpp launch: an event on the old stream): one context
+    alternating two streams with no host synchronisation renders every frame
+    equal to a fresh render of it, though the frames share its pixel state."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    bg, arr = textures
+    scene = sc.scene_default(textured=True)
+    cams = [sc.random_camera(700 + i) for i in range(6)]
+    params = abi.default_params(max_steps=500, percent_black=-1.0)
+    W, H = 160, 90
+    r = pkg.Renderer(0)
+    r.set_scene(scene)
+    r.set_background(bg)
+    r.set_texture_array(arr)
+    ref = [r.render(c, params, W, H).cpu().numpy() for c in cams]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    got = []
+    for rep in range(2):
+        for i, c in enumerate(cams):
+            s = streams[(i + rep) % 2]
+            with torch.cuda.stream(s):
+                got.append((i, r.render(c, params, W, H, stream=s)))
+    torch.cuda.synchronize()
+    for i, out in got:
+        assert np.array_equal(out.cpu().numpy(), ref[i]), i
+    assert r.diag_counters() == {"hit_not_opaque": 0, "free_errors": 0}
+    r.close()
+
+
+def test_zz_diag_counters_zero(gpu):
+    """After every render of this module on the shared context (translucent,
+    single-sided and textured materials, stress scenes, resumed rays): no
+    pixel stopped at an opaque-classified hit whose shaded alpha was not 1
+    (the step loop's classification is exact where it claims), and no
+    stream-ordered free failed."""
+    assert gpu.diag_counters() == {"hit_not_opaque": 0, "free_errors": 0}

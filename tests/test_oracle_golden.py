@@ -5,24 +5,19 @@ SwiftShader 4.1 (tests/golden/make_golden.py).
 Tolerance budget. SwiftShader's texture filter, sin/atan/asin
 and interpolation of `uv` are one valid GL implementation, not bit-defined:
   - untextured scenes:   >= 99.9 % of pixels within 2/255 per channel and
-                          every pixel within 4/255; the far-camera reseed
-                          goldens only: at most 0.05 % beyond 4/255 (SURVEY
-                          §7 hard part 1: rays that orbit the photon ring for
-                          hundreds of steps leave in a direction that differs
-                          in the last bits and may cross a skybox checker
-                          edge; 1-4 pixels, equal step counts); executed step
-                          counts equal on >= 99.9 % of pixels. The
-                          headline-size bands (golden_r3.npz) are photon-ring
-                          rays of up to 1,900 (4,000) steps and take that
-                          allowance too: one pixel of 30,720 in rows 704-719,
-                          5/255 after 1,237 equal steps; step counts equal on
-                          99.97 %. The
-                          material-flag goldens (translucent textured
-                          surfaces, normal maps) take the same 0.05 %
-                          allowance: a ray through several translucent
-                          surfaces sums several of SwiftShader's fixed-point
-                          filter results (one pixel of features_low, 5/255,
-                          equal step counts);
+                          every pixel within 4/255, except the named pixel
+                          counts of ALLOW_GT4 (measured, exact: a regression
+                          elsewhere cannot hide in them). The far-camera
+                          reseed goldens (SURVEY §7 hard part 1: rays that
+                          orbit the photon ring for hundreds of steps leave in
+                          a direction that differs in the last bits and may
+                          cross a skybox checker edge; 1-4 pixels); the
+                          headline-size band of rows 704-719 (one pixel of
+                          30,720, 5/255 after 1,237 equal steps); features_low
+                          (a ray through several translucent surfaces sums
+                          several of SwiftShader's fixed-point filter results:
+                          one pixel, 5/255, equal step counts). Executed step
+                          counts equal on >= 99.9 % of pixels;
   - textured scenes:     SwiftShader samples RGBA8 in 16-bit fixed point, so an
                           opaque texel reads alpha 65527..65531/65535 < 1 and
                           the ray does not stop at textured objects
@@ -57,6 +52,13 @@ R2_BUDGET = RESEED + ["config2_640x360"] + FEATURES
 # at full frame size under a scissor rectangle
 BANDS_UNTEX = ["band1080_704_untex", "band1080_536_untex", "band2160_1408_untex"]
 BANDS_TEX = ["band1080_704_tex", "band1080_536_tex"]
+# The only pixels allowed beyond 4/255, by case (every other case: none). The
+# counts are what the oracle gives against SwiftShader today; each is
+# explained in the module docstring.
+ALLOW_GT4 = {"reseed_r120": 4, "reseed_r300": 2, "reseed_side": 1, "features_low": 1, "band1080_704_untex": 1,
+             "band1080_704_tex": 1}
+# float FragColor pixels allowed at >= 0.02 from SwiftShader's, by case
+ALLOW_F32 = {"reseed_r120": 2}
 
 
 @pytest.fixture(scope="module")
@@ -101,10 +103,8 @@ def test_untextured_within_budget(pkg, oracle, golden, tex, name):
     rgba8, _, steps, ref = run(pkg, oracle, golden, tex, name)
     d = np.abs(rgba8.astype(int) - ref.astype(int)).max(-1)
     assert np.mean(d <= 2) >= 0.999, (name, np.mean(d <= 2))
-    if name in RESEED + FEATURES + BANDS_UNTEX:  # ring rays, far cameras, stacked translucent lookups (docstring)
-        assert np.mean(d > 4) <= 5e-4, (name, int((d > 4).sum()), d.max())
-    else:
-        assert d.max() <= 4, (name, int((d > 4).sum()), d.max())
+    # ring rays, far cameras, stacked translucent lookups: the named pixels only (docstring)
+    assert int((d > 4).sum()) <= ALLOW_GT4.get(name, 0), (name, int((d > 4).sum()), d.max())
     if name + "/steps" in golden:
         assert np.mean(golden[name + "/steps"].astype(int) == steps) >= 0.999
 
@@ -118,10 +118,7 @@ def test_float_fragcolor(pkg, oracle, golden, tex, name):
     ref = golden[name + "/rgba32"]
     d = np.abs(rgba32 - ref)
     assert np.median(d) < 2e-4
-    if name in RESEED + FEATURES:
-        assert np.mean(d.max(-1) >= 0.02) <= 5e-4, (name, int((d.max(-1) >= 0.02).sum()), d.max())
-    else:
-        assert d.max() < 0.02, (name, int((d.max(-1) >= 0.02).sum()), d.max())
+    assert int((d.max(-1) >= 0.02).sum()) <= ALLOW_F32.get(name, 0), (name, int((d.max(-1) >= 0.02).sum()), d.max())
 
 
 @pytest.mark.parametrize("name", TEXTURED + BANDS_TEX)
@@ -136,10 +133,8 @@ def test_textured_pinned_where_alpha_semantics_agree(pkg, oracle, golden, tex, n
     # the small frames: more rays SwiftShader lets through (alpha < 1)
     assert same.mean() >= (0.6 if name in BANDS_TEX else 0.75), same.mean()
     assert np.mean(d[same] <= 2) >= 0.999
-    if name in BANDS_TEX:  # photon-ring rays of the untextured allowance
-        assert np.mean(d[same] > 4) <= 5e-4, (name, int((d[same] > 4).sum()))
-    else:
-        assert d[same].max() <= 4
+    # photon-ring rays of the untextured allowance (named pixels only)
+    assert int((d[same] > 4).sum()) <= ALLOW_GT4.get(name, 0), (name, int((d[same] > 4).sum()))
 
 
 def test_noise_mask_statistics(pkg, oracle, golden, tex):
