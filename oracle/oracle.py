@@ -55,10 +55,27 @@ def load() -> C.CDLL:
         lib.sro_pressr_sweep.restype = C.c_int64
         lib.sro_pressr_sweep.argtypes = [C.POINTER(abi.Camera), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_int]
+        lib.sro_sample_texture.restype = C.c_int
+        lib.sro_sample_texture.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
+                                           C.POINTER(C.c_float)]
         lib.sro_pressr_ray_repeat.restype = C.c_int
         lib.sro_pressr_ray_repeat.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), C.c_int, C.c_int, C.c_int]
         _lib = lib
     return _lib
+
+
+# filter_mode of the oracle only: SwiftShader 4.1's fixed-point sampler (test infrastructure)
+FILTER_SWIFTSHADER = 2
+
+
+def sample_texture(img: np.ndarray, u: float, v: float, mode: int) -> np.ndarray:
+    """One texture() lookup of the oracle's sampler on an [H, W, C] uint8 image."""
+    a = np.ascontiguousarray(img, dtype=np.uint8)
+    out = (C.c_float * 4)()
+    rc = load().sro_sample_texture(a.ctypes.data, a.shape[1], a.shape[0], a.shape[2], float(u), float(v), int(mode),
+                                   out)
+    assert rc == 0
+    return np.frombuffer(out, dtype=np.float32).copy()
 
 
 class TextureSet:

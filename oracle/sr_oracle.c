@@ -151,9 +151,62 @@ static v4 wsum4(v4 t00, v4 t10, v4 t01, v4 t11, float a, float b) {
               ((t00.z * w00 + t10.z * w10) + t01.z * w01) + t11.z * w11,
               ((t00.w * w00 + t10.w * w10) + t01.w * w01) + t11.w * w11);
 }
+/* SwiftShader 4.1's GL_LINEAR + GL_REPEAT sampler of an RGBA8 / RGB8 texture
+ * (test only: the filter the golden renders ran with; the library has no
+ * such mode). Measured on the SwiftShader of this image with a probe shader
+ * of our own over random textures (POT and NPOT, array and 2D, RGB and RGBA)
+ * and coordinates, bit-exact on every sample
+ * (tests/golden/probe_swiftshader_filter.py):
+ *   - the coordinate is a 0.16 fixed-point fraction of the texture: U =
+ *     trunc(float32(x * 65536)) (x86 truncation: out of range -> low bits 0),
+ *     minus half a texel 0x8000 / n, mod 2^16; texel i0 = (U0 n) >> 16 with
+ *     fraction f = (U0 n) mod 2^16, texel i1 from U0 + 2 (0x8000 / n) the
+ *     same way (so i1 == i0 when f is small on an NPOT size);
+ *   - texels widen to 16 bits (c * 257); weights MulHigh(~f_u or f_u, ~f_v or
+ *     f_v) with ~f = 0xFFFF - f, MulHigh(a, b) = (a b) >> 16; the result
+ *     (MulHigh(c00, w00) + MulHigh(c10, w10)) + (MulHigh(c01, w01) +
+ *     MulHigh(c11, w11)) is a UNORM16, returned as float32(K) * (1 / 65535);
+ *   - a 3-channel texture reads alpha 1.0.
+ * An opaque texel therefore reads alpha 65527..65533 / 65535 < 1: the
+ * reference's `alpha == 1.` (frag:932) never stops a ray at a textured
+ * object there. */
+static int ss_coord(float x, int n, int* i0, int* i1) {
+    const float xf = x * 65536.0f;
+    const uint32_t U = fabsf(xf) < 2147483648.0f ? (uint32_t)(int32_t)xf : 0x80000000u;  /* truncation */
+    const uint32_t U0 = (U - (uint32_t)(0x8000 / n)) & 0xFFFFu;
+    const uint32_t U1 = (U0 + 2u * (uint32_t)(0x8000 / n)) & 0xFFFFu;  /* one texel: twice the half */
+    const uint32_t p = U0 * (uint32_t)n;
+    *i0 = (int)(p >> 16);
+    *i1 = (int)((U1 * (uint32_t)n) >> 16);
+    return (int)(p & 0xFFFFu);
+}
+static uint32_t ss_mh(uint32_t a, uint32_t b) { return (a * b) >> 16; }
+static v4 sample_swiftshader(const uint8_t* base, int w, int h, int ch, float u, float v) {
+    int x0, x1, y0, y1;
+    const uint32_t fu = (uint32_t)ss_coord(u, w, &x0, &x1), fv = (uint32_t)ss_coord(v, h, &y0, &y1);
+    const uint32_t nfu = 0xFFFFu - fu, nfv = 0xFFFFu - fv;
+    const uint32_t w00 = ss_mh(nfu, nfv), w10 = ss_mh(fu, nfv), w01 = ss_mh(nfu, fv), w11 = ss_mh(fu, fv);
+    const uint8_t* t00 = base + ((size_t)y0 * (size_t)w + (size_t)x0) * (size_t)ch;
+    const uint8_t* t10 = base + ((size_t)y0 * (size_t)w + (size_t)x1) * (size_t)ch;
+    const uint8_t* t01 = base + ((size_t)y1 * (size_t)w + (size_t)x0) * (size_t)ch;
+    const uint8_t* t11 = base + ((size_t)y1 * (size_t)w + (size_t)x1) * (size_t)ch;
+    float r[4];
+    for (int k = 0; k < 4; k++) {
+        if (k == 3 && ch < 4) {
+            r[k] = 1.0f;
+            continue;
+        }
+        const uint32_t K = (ss_mh(t00[k] * 257u, w00) + ss_mh(t10[k] * 257u, w10)) +
+                           (ss_mh(t01[k] * 257u, w01) + ss_mh(t11[k] * 257u, w11));
+        r[k] = (float)K * (1.0f / 65535.0f);
+    }
+    return V4(r[0], r[1], r[2], r[3]);
+}
+
 /* GL_LINEAR + GL_REPEAT, texel centres at (i + 1/2) / size, no mipmaps. A
  * non-finite or out-of-range coordinate reads texel 0 (GLSL leaves it undefined). */
 static v4 sample_bilinear(const uint8_t* base, int w, int h, int ch, float u, float v, int mode) {
+    if (mode == SRO_FILTER_SWIFTSHADER) return sample_swiftshader(base, w, h, ch, u, v);
     float s = u * (float)w - 0.5f;
     float t = v * (float)h - 0.5f;
     if (!(fabsf(s) < 16777216.0f)) s = 0.0f;
@@ -166,6 +219,16 @@ static v4 sample_bilinear(const uint8_t* base, int w, int h, int ch, float u, fl
     v4 t01 = fetch_texel(base, w, ch, x0, y1), t11 = fetch_texel(base, w, ch, x1, y1);
     if (mode == SR_FILTER_WEIGHTED) return wsum4(t00, t10, t01, t11, a, b);
     return lerp4(lerp4(t00, t10, a), lerp4(t01, t11, a), b);
+}
+int sro_sample_texture(const uint8_t* base, int width, int height, int channels, float u, float v, int mode,
+                       float out_rgba[4]) {
+    if (!base || width <= 0 || height <= 0 || (channels != 3 && channels != 4) || !out_rgba) return -1;
+    const v4 r = sample_bilinear(base, width, height, channels, u, v, mode);
+    out_rgba[0] = r.x;
+    out_rgba[1] = r.y;
+    out_rgba[2] = r.z;
+    out_rgba[3] = r.w;
+    return 0;
 }
 static v4 texture_bg(const Ctx* c, v2 uv) {
     const sro_textures* t = c->tex;

@@ -29,6 +29,12 @@
 extern "C" {
 #endif
 
+/* params->filter_mode of the oracle only (test infrastructure): SwiftShader
+ * 4.1's fixed-point RGBA8 sampler (sr_oracle.c sample_swiftshader), the
+ * filter the golden renders ran with. The library accepts SR_FILTER_LERP and
+ * SR_FILTER_WEIGHTED only. */
+#define SRO_FILTER_SWIFTSHADER 2
+
 typedef struct {
     const uint8_t* bg; /* skybox, rows bottom-up, NULL = incomplete texture */
     int bg_w, bg_h, bg_channels;
@@ -42,6 +48,12 @@ int sro_render(const sr_scene* scene, const sr_test_ray* test_ray, const sro_tex
                const sr_camera* cam, const sr_params* params, int width, int height,
                int row_begin, int row_end, uint8_t* rgba8, float* rgba32, int32_t* steps,
                int nthreads);
+
+/* One texture() lookup of the oracle's sampler (GL_LINEAR + GL_REPEAT) on
+ * one RGBA8 / RGB8 image (rows bottom-up), mode SR_FILTER_* or
+ * SRO_FILTER_SWIFTSHADER. 0, or -1 on bad arguments. */
+int sro_sample_texture(const uint8_t* base, int width, int height, int channels, float u, float v, int mode,
+                       float out_rgba[4]);
 
 /* One pixel (px, py), GL order. Returns the number of executed steps. */
 int sro_shade_pixel(const sr_scene* scene, const sr_test_ray* test_ray, const sro_textures* tex,

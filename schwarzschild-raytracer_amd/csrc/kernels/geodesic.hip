@@ -900,7 +900,8 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 template <int NB>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
-                                                 bool outward, float dip, bool bhx, bool bh_ok, bool falling) {
+                                                 bool outward, float dip, float dphi, bool bhx, bool bh_ok,
+                                                 bool falling) {
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
@@ -987,9 +988,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     SR_PTB(3);
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
-    float dipv = dip;
-    asm volatile("" : "+v"(dipv));  // computed here: hoisted out of the step loop it was a spilled VGPR
-    const float dphi = __builtin_amdgcn_sqrtf(8.0f * (1.0f - dipv));  // >= the step angle (sr_dev_frame.out_dip)
     uint32_t reach = 0;
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
@@ -2228,7 +2226,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event<NB>(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                     bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
+                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
