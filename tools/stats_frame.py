@@ -101,6 +101,14 @@ def main():
     out["wave_us_max"] = round(float((e_ - s_).max()), 1)
     out["last_start_us"] = round(float(s_.max()), 1)
     out["busy_frac"] = round(float((e_ - s_).sum() / (span * max(active))), 3)
+    # in-kernel shader clock (rec[15]: s_memtime cycles of the wave over its
+    # s_memrealtime span at 100 MHz; MI355X_MICROARCH.md DVFS item 6). Use an
+    # SR_STATS_NOCOUNT build: the counters' atomics distort the timeline.
+    ok = (t[:, 15] > 0) & (e_ - s_ > 50.0)
+    if ok.any():
+        ghz = t[ok, 15] / ((e_ - s_)[ok] * 1e3)
+        out["clock_ghz"] = {"median": round(float(np.median(ghz)), 3), "p10": round(float(np.percentile(ghz, 10)), 3),
+                            "p90": round(float(np.percentile(ghz, 90)), 3), "waves": int(ok.sum())}
     dur = e_ - s_
     top = np.argsort(-dur)[:8]
     gx = (1920 + 15) // 16
