@@ -156,8 +156,9 @@ def parse():
                     help="rows of the frame swept on the CPU for `value` (0 = every row: the full frame)")
     ap.add_argument("--single-frame", choices=["on", "off"], default="on",
                     help="also time single-frame launches (N = 1): one frame alone, and 4 in flight")
-    ap.add_argument("--single-split", default="0",
-                    help="split tiles for the single-frame figures: max_tiles[:lanes[:min_steps]] (0 = off)")
+    ap.add_argument("--single-split", default="64:16:1000",
+                    help="split tiles for the latency figure of one frame alone: max_tiles[:lanes[:min_steps]] "
+                         "(0 = off; the costliest tiles' rays in sparse waves, DESIGN.md §6)")
     ap.add_argument("--dump-frames", default="",
                     help="directory: rank 0 saves every timed frame as assembled (frame_<f>.npy), for the "
                          "multi-rank parity test; copies are taken after the timed region")
@@ -259,8 +260,10 @@ def main():
     def keep(first, batch):
         if batch is None:
             return
-        # FrameGather reuses its frame buffer at its next call: keep a copy
-        last[0] = (first, batch.clone() if hasattr(batch, "clone") else batch)
+        # no copy: FrameGather reuses its frame buffer at its NEXT call, and the
+        # parity check reads this (the last launch's) before any further launch
+        # (a copy here, in the timed region, cost ~7 % of the headline: s2)
+        last[0] = (first, batch)
         if args.dump_frames:
             for i in range(batch.shape[0]):
                 if first + i >= dump_from[0]:
@@ -622,27 +625,41 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
         extra.append(rk)
         pool.append((rk, torch.zeros((1,) + tuple(ctxs[0][1].shape[1:]), dtype=torch.uint8, device=dev),
                      torch.cuda.Stream(dev)))
-    for rk, _, _ in pool:
-        rk.set_split(split[0], split[1], split[2])
     n_cam = len(cams)
-    # each context learns the single-frame launch order (and split tiles) first
-    for k, (rk, tile_k, s_k) in enumerate(pool):
-        with torch.cuda.stream(s_k):
-            for j in range(2):
-                render(rk, (first + k + j) % n_cam, 1, tile_k, s_k)
-    for _, _, s_k in pool:
-        s_k.synchronize()
-    rk, tile_k, s_k = pool[0]
-    times = []
-    for j in range(alone_reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        with torch.cuda.stream(s_k):
-            e0.record(s_k)
-            render(rk, (first + j) % n_cam, 1, tile_k, s_k)
-            e1.record(s_k)
-        s_k.synchronize()
-        times.append(e0.elapsed_time(e1))
-    alone = statistics.median(times)
+
+    def learn(sp):  # each context learns the single-frame launch order (and split tiles) first
+        for rk, _, _ in pool:
+            rk.set_split(*sp)
+        for k, (rk, tile_k, s_k) in enumerate(pool):
+            with torch.cuda.stream(s_k):
+                for j in range(2):
+                    render(rk, (first + k + j) % n_cam, 1, tile_k, s_k)
+        for _, _, s_k in pool:
+            s_k.synchronize()
+
+    def one_alone():
+        rk, tile_k, s_k = pool[0]
+        times = []
+        for j in range(alone_reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            with torch.cuda.stream(s_k):
+                e0.record(s_k)
+                render(rk, (first + j) % n_cam, 1, tile_k, s_k)
+                e1.record(s_k)
+            s_k.synchronize()
+            times.append(e0.elapsed_time(e1))
+        return statistics.median(times)
+
+    # the latency mode (sr_set_latency_mode: 2-step fast loop) with split tiles,
+    # then the default kernel without them
+    for rk, _, _ in pool:
+        rk.set_latency_mode(True)
+    learn(split)
+    alone = one_alone()
+    for rk, _, _ in pool:
+        rk.set_latency_mode(False)
+    learn((0, 16, 1))
+    alone_unsplit = one_alone()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for j in range(frames):
@@ -659,10 +676,13 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
         rk.close()
     return {
         "alone": {"frames_per_launch": 1, "launches_in_flight": 1, "ms_per_frame": round(alone, 4),
-                  "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events"},
+                  "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events",
+                  "split_tiles": split_arg, "latency_mode": True},
+        "alone_default": {"ms_per_frame": round(alone_unsplit, 4), "mpix_s": round(W * H / alone_unsplit / 1e3, 3),
+                          "split_tiles": "0", "latency_mode": False},
         "inflight": {"frames_per_launch": 1, "launches_in_flight": inflight, "ms_per_frame": round(per, 4),
-                     "mpix_s": round(W * H / per / 1e3, 3), "frames": frames, "stat": "wall clock"},
-        "split_tiles": split_arg,
+                     "mpix_s": round(W * H / per / 1e3, 3), "frames": frames, "stat": "wall clock",
+                     "split_tiles": "0"},
     }
 
 

@@ -371,6 +371,14 @@ int sr_render_debug(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, 
  * tiles. max_tiles 0 (the default) turns it off. */
 int sr_set_split(sr_ctx* ctx, int max_tiles, int lanes_per_wave, int min_steps);
 
+/* Latency mode (not in the reference; the pixels are unchanged): on != 0 runs
+ * the next frames' step loop with two fast-loop steps per iteration instead of
+ * three: one frame alone finishes ~5 % sooner (its longest rays' dependency
+ * chain), frames in flight run ~0.5 % slower. For an interactive caller that
+ * draws one frame at a time (src/main.cpp:318-319); pair it with sr_set_split
+ * (the costliest tiles' rays in sparse waves). Off by default. */
+int sr_set_latency_mode(sr_ctx* ctx, int on);
+
 /* Rows a sr_render_blocks call with these arguments writes. */
 int sr_blocks_row_count(int height, int block_rows, int block_first, int block_step);
 

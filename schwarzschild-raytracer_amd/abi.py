@@ -187,6 +187,7 @@ SIGNATURES = {
     "sr_render_debug": (_i, [_p, C.POINTER(Camera), C.POINTER(Params), _i, _i, _i, _i, _p, _p, _p, _p]),
     "sr_blocks_row_count": (_i, [_i, _i, _i, _i]),
     "sr_set_split": (_i, [_p, _i, _i, _i]),
+    "sr_set_latency_mode": (_i, [_p, _i]),
     "sr_write_png": (_i, [C.c_char_p, _p, _i, _i, C.c_size_t, _i]),
     "sr_render_blocks_batch": (_i, [_p, C.POINTER(Camera), _i, C.POINTER(Params), _i, _i, _i, _i, _i, _p,
                                     C.c_size_t, C.c_size_t, _p]),

@@ -156,6 +156,7 @@ typedef struct {
     float res_x, res_y; // resolution uniform == frame size
     float u_f;
     float uf_radius;    // 1 / u_f (frag:893)
+    float uf_radius2;   // uf_radius * uf_radius in binary32 (sphere_intersect's r * r, frag:461)
     float percent_black;
     float curved_percentage;
     int32_t max_steps;
@@ -197,6 +198,10 @@ typedef struct {
     // sqrt(8 (1 - out_dip)), rounded up: at least the step angle (the budget
     // events' directional plane window, geodesic.hip plane_window)
     float max_dphi;
+    // fast-loop steps per iteration of the integrate kernel: 3, or 2 in the
+    // latency mode (sr_set_latency_mode: one frame alone ~5 % sooner, frames
+    // in flight ~0.5 % slower)
+    int32_t fast_unroll;
 } sr_dev_frame;
 
 #endif

@@ -151,11 +151,12 @@ __device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
 #endif
 
 // ---- primitive tests: return the reference's is_hit and fill p ------------
-// sphere_intersect, frag:457-478
-__device__ __forceinline__ bool sphere_test(f3 o, f3 d, f3 c, float r, float max_lambda, f3& p) {
+// sphere_intersect, frag:457-478 (r2: the float square r * r of the radius):
+// whether it hits, and its lambda (the point is o + d * lam, sphere_test_r2)
+__device__ __forceinline__ bool sphere_lambda_r2(f3 o, f3 d, f3 c, float r2, float max_lambda, float& lam_out) {
     f3 oc = o - c;
     float b = dot(d, oc);
-    float D = b * b - dot(oc, oc) + r * r;
+    float D = b * b - dot(oc, oc) + r2;
     if (D < 0.0f) return false;
     float sq = sqrtf(D);
     float first = -dot(d, oc);
@@ -164,9 +165,17 @@ __device__ __forceinline__ bool sphere_test(f3 o, f3 d, f3 c, float r, float max
     if (l1 > 0.0f && l2 > 0.0f) lam = gmin(l1, l2);
     else if (l1 > 0.0f) lam = l1;
     else if (l2 > 0.0f) lam = l2;
-    bool hit = lam >= 0.0f && (max_lambda < 0.0f || lam <= max_lambda);
+    lam_out = lam;
+    return lam >= 0.0f && (max_lambda < 0.0f || lam <= max_lambda);
+}
+__device__ __forceinline__ bool sphere_test_r2(f3 o, f3 d, f3 c, float r2, float max_lambda, f3& p) {
+    float lam;
+    const bool hit = sphere_lambda_r2(o, d, c, r2, max_lambda, lam);
     if (hit) p = o + d * lam;
     return hit;
+}
+__device__ __forceinline__ bool sphere_test(f3 o, f3 d, f3 c, float r, float max_lambda, f3& p) {
+    return sphere_test_r2(o, d, c, r * r, max_lambda, p);
 }
 
 // plane_intersect, frag:483-500 (normal = axes[1])
@@ -364,6 +373,11 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 #ifndef SR_NEAR
 #define SR_NEAR 1.0f
 #endif
+#ifndef SR_XPLANE  // orbital-plane exclusion of bounded slots (budget_frame)
+#define SR_XPLANE 1
+#endif
+// |o|_1 + len + 1 of a chord whose ends lie within r = 110: sqrt(3) 110 + 220 + 1 <= 412
+#define SR_XPLANE_S 420.0f
 // The margin factor of a slot's distance tests: a planar primitive's
 // per-chord factor (SR_MU_PLANAR: it accepts a chord point within a few eps
 // S of its plane and bounds), the quadratic one for spheres and cylinders
@@ -548,8 +562,11 @@ __device__ __forceinline__ float clearance_slab(const sr_dev_slot& sl, f3 A, flo
     return ey - sl.mp - 1.8f * SR_MU_QUADRATIC * a;
 }
 
-// NaN-propagating minimum: a NaN clearance must force the exact tests.
-__device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e : m; }
+// NaN-propagating minimum: a NaN clearance must force the exact tests. IEEE
+// minimum (v_minimum3_f32 on gfx950): NaN if either operand is NaN, one
+// instruction (the select form it replaces, `!(e >= m) ? e : m`, took two and
+// dropped an earlier NaN when a later operand was a number).
+__device__ __forceinline__ float nmin(float m, float e) { return __builtin_elementwise_minimum(m, e); }
 
 // Per-lane budget state: E[j] = clearance_j(anchor_j) - slacked path from
 // anchor_j to the last budget event, T = slacked path since that event,
@@ -576,7 +593,8 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
-#ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries)
+#ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries);
+                        // the latency mode's instantiation runs 2 (sr_set_latency_mode)
 #define SR_FAST_UNROLL 3
 #endif
 #ifndef SR_AHEAD_T
@@ -587,7 +605,17 @@ __device__ __forceinline__ float nmin(float m, float e) { return !(e >= m) ? e :
 #endif
 #define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
 #define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
-#define SR_E_ROWS (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
+// the budget's per-lane scalars (Budget::T() ... cm()): not needed inside
+// the fast loop, so they wait in LDS instead of registers (held in VGPRs
+// across it they were spilled to scratch and reloaded at every event)
+#define SR_E_BT (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
+#define SR_E_BM (SR_E_BT + 1)
+#define SR_E_BCX (SR_E_BT + 2)
+#define SR_E_BCY (SR_E_BT + 3)
+#define SR_E_BMH (SR_E_BT + 4)
+#define SR_E_BCM (SR_E_BT + 5)
+#define SR_E_BUHI (SR_E_BT + 6)
+#define SR_E_ROWS (SR_E_BT + 7)
 // The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
 // the step's angle dphi at the origin, so it stays in the half-plane beyond
@@ -660,17 +688,41 @@ __device__ __forceinline__ float ball_q(float R, float cx, float cy) {
 
 struct Budget {
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
-    float T, m;
-#if SR_BALL
-    float cx, cy;  // the ball's centre: the last event's end point in the orbital plane (nv, tv)
-#endif
-    float uhi;  // the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; SR_BH_U2:
-                // the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo())
-    __device__ __forceinline__ float ulo(float u_f) const { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
-    uint32_t cm;  // budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
-    float mh;     // min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound that
-                  // covers chords nearly parallel to an axis
     int pa0, slab0;  // LDS rows of pa[0] and H[0] (SR_E_PA0 / SR_E_SLAB0)
+    // Scalars in LDS rows (SR_E_BT ..), read with volatile loads so that no
+    // register holds them across the fast loop:
+    //   T   the charge since the last event (slacked path; SR_BALL: displacement)
+    //   m   min_j E[j]
+    //   cx, cy  SR_BALL: the ball's centre, the last event's end point in the orbital plane (nv, tv)
+    //   mh  min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound
+    //       that covers chords nearly parallel to an axis
+    //   cm  budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
+    //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; SR_BH_U2:
+    //       the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo_of())
+    __device__ __forceinline__ float ld(int row) const { return E[row * SR_E_STRIDE]; }
+    __device__ __forceinline__ void st(int row, float v) const { E[row * SR_E_STRIDE] = v; }
+    __device__ __forceinline__ float T() const { return ld(SR_E_BT); }
+    __device__ __forceinline__ void setT(float v) const { st(SR_E_BT, v); }
+    __device__ __forceinline__ float m() const { return ld(SR_E_BM); }
+    __device__ __forceinline__ void setM(float v) const { st(SR_E_BM, v); }
+    __device__ __forceinline__ float cx() const { return ld(SR_E_BCX); }
+    __device__ __forceinline__ float cy() const { return ld(SR_E_BCY); }
+    __device__ __forceinline__ void setC(float x, float y) const {
+        st(SR_E_BCX, x);
+        st(SR_E_BCY, y);
+    }
+    __device__ __forceinline__ float mh() const { return ld(SR_E_BMH); }
+    __device__ __forceinline__ void setMh(float v) const { st(SR_E_BMH, v); }
+    // the SR_E_BCM row holds cm in bits 0..7 and the orbit's excluded slots
+    // (bit 8 + j: slot j, budget_frame) above
+    __device__ __forceinline__ uint32_t cm() const { return __float_as_uint(ld(SR_E_BCM)) & 0xffu; }
+    __device__ __forceinline__ uint32_t excl() const { return __float_as_uint(ld(SR_E_BCM)) >> 8; }
+    __device__ __forceinline__ void setCm(uint32_t cm, uint32_t excl) const {
+        st(SR_E_BCM, __uint_as_float(cm | (excl << 8)));
+    }
+    __device__ __forceinline__ float uhi() const { return ld(SR_E_BUHI); }
+    __device__ __forceinline__ void setUhi(float v) const { st(SR_E_BUHI, v); }
+    static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -701,43 +753,73 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
             c &= c - 1;
         }
     }
-    bs.cm = cm;
+    uint32_t x = 0;
+#if SR_XPLANE
+    // Orbital-plane exclusion (per orbit): every chord of this orbit joins two
+    // end points (nv cos phi + tv sin phi) / u computed in binary32, within
+    // 4e-7 r of the plane span(nv, tv) through the origin, and an object's
+    // exact test accepts only points within br + mu S of its bounding
+    // sphere's centre bc (may_hit). So when bc lies farther from that plane
+    // than br + mu S_max (S_max = SR_XPLANE_S bounds |o|_1 + len + 1 for chords
+    // whose ends lie within r = 110, the u_f sphere's exit chords included,
+    // as outward_clear assumes) plus the rounding, no chord of the orbit can
+    // reach the object: its budget is +inf until the next reseed (a new
+    // plane). Planes (unbounded) and cylinders (their quadratic margin grows
+    // near the axis direction) are never excluded. Of the default scene the
+    // sphere and the box lie off most rays' planes (the pencil of planes
+    // through the camera and the hole).
+    {
+        const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
+        const float nn = dot(n, n);
+        const int nb = sc->num_budget;
+        for (int j = 1; j <= nb; j++) {
+            const sr_dev_slot& sl = sc->slots[j - 1];
+            if (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_CYLINDER) continue;
+            const float h = dot(ld3(sl.bc), n);  // |h| / |n|: bc's distance from the plane
+            const float need = (sl.br + sl.mu * SR_XPLANE_S) * 1.001f + 1.0e-4f + 1.0e-5f * sl.cn;
+            // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
+            x |= (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
+        }
+    }
+#endif
+    bs.setCm(cm, x);
 }
 
 // bs.cm's bit for slot j (budgeted cylinders; false for other slots)
 __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc, const Budget& bs, int j) {
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;
     if (!((cyl >> (j - 1)) & 1u)) return false;
-    return (bs.cm >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
+    return (bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
 }
 
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
-    bs.T = 0.0f;
+    bs.setT(0.0f);
 #if SR_BALL
     // the ball's centre: A in the orbital plane (A lies in it: the camera, or a
     // chord end point), within 1e-6 a of A; the budgets give that up
-    bs.cx = dot(A, nv);
-    bs.cy = dot(A, tv);
+    bs.setC(dot(A, nv), dot(A, tv));
     const float m0 = 2.0e-6f * (a + 1.0f);
 #else
     const float m0 = 0.0f;
 #endif
     float m = INFINITY;
     budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
+    const uint32_t xcl = bs.excl();
     {
         float e = clearance_bh(a);
-        bs.uhi = INFINITY;
+        float uhi = INFINITY;
         if (SR_BH_WINDOW && bh_ok && a > SR_BH_RWIN) {
             e = INFINITY;
-            bs.uhi = SR_BH_U;
+            uhi = SR_BH_U;
         }
         if (SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a > SR_BH_RWIN2 && a < SR_BH_RMAX2 && (falling || !(a > SR_BH_RWIN))) {
             e = INFINITY;
-            bs.uhi = SR_BH_U2;
+            uhi = SR_BH_U2;
         }
+        bs.setUhi(uhi);
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
         e -= m0;
         bs.E[0] = e;
@@ -748,10 +830,11 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);  // one batch of scalar loads per slot
         float e = clearance_obj(sl, A, a) - m0;
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
+        if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
     }
-    bs.m = m;
+    bs.setM(m);
     float mh = INFINITY;
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
 #pragma unroll
@@ -763,7 +846,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
             c &= c - 1;
         }
     }
-    bs.mh = mh;
+    bs.setMh(mh);
 }
 
 // The orbit's (pa, pb) on each budgeted cylinder's axis (budget_frame),
@@ -905,7 +988,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
-    const float T = bs.T;
+    const float T = bs.T();
     float e[NS], h[SR_MAX_CYLINDERS];
 #pragma unroll
     for (int j = 0; j < NS; j++) e[j] = bs.E[j * SR_E_STRIDE];
@@ -936,12 +1019,10 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     }
     if (reanchor_cyl) forced |= (2u << nb) - 1u;  // a new orbital frame: outward budgets start over
     uint32_t spent = 0;  // wave-uniform: slots some lane has spent or is about to
-    uint32_t hard = forced;  // this lane's slots whose budget does not cover the chord
     // one ballot per slot of a single compare (written straight to an SGPR
     // pair); forced slots, rare (reseeds, near-axis chords), balloted apart
 #pragma unroll
     for (int j = 0; j < NS; j++) {
-        hard |= (uint32_t)!(T < e[j]) << j;
         if (__ballot(!(T + ahead < e[j]))) spent |= 1u << j;
     }
     if (__ballot(forced != 0u)) {
@@ -989,6 +1070,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
+    const uint32_t xcl = SR_XPLANE ? bs.excl() : 0u;  // slots off this orbit's plane (budget_frame)
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
         SR_STAT(14 + j, 1);
@@ -997,14 +1079,15 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
 #endif
         // only lanes whose budget did not cover the chord can reach the slot
         // (the others re-anchor early: look-ahead, or another lane spent it)
-        const bool h = (hard >> j) & 1u;
+        // (its E is still the uncharged one in LDS: spent slots are only written below)
+        const bool h = ((forced >> j) & 1u) || !(T < bs.E[j * SR_E_STRIDE]);
         if (j == 0) {
             // beyond the band: the u window instead of a distance budget
             const bool win1 = SR_BH_WINDOW && bh_ok && a - perr > SR_BH_RWIN;
             const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a - perr > SR_BH_RWIN2 && a + perr < SR_BH_RMAX2 &&
                               (falling || !win1);
             const bool win = win1 || win2;
-            bs.uhi = win2 ? SR_BH_U2 : win1 ? SR_BH_U : INFINITY;
+            bs.setUhi(win2 ? SR_BH_U2 : win1 ? SR_BH_U : INFINITY);
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
@@ -1034,9 +1117,10 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             }
             if (TY != SR_OBJECT_PLANE && outward &&
                 outward_slot(st, TY == SR_OBJECT_CYLINDER &&
-                                     ((bs.cm >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
+                                     ((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
                              a, dip))
                 v = INFINITY;
+            if (TY != SR_OBJECT_PLANE && TY != SR_OBJECT_CYLINDER && ((xcl >> j) & 1u)) v = INFINITY;  // budget_frame
             bs.E[j * SR_E_STRIDE] = v;
             m = nmin(m, v);
             if (TY == SR_OBJECT_CYLINDER) {
@@ -1057,9 +1141,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         default: reanchor(std::integral_constant<int, SR_OBJECT_SPHERE>{}); break;
         }
     }
-    bs.T = 0.0f;
-    bs.m = m;
-    bs.mh = mh;
+    bs.setT(0.0f);
+    bs.setM(m);
+    bs.setMh(mh);
     return reach;
 }
 
@@ -1699,7 +1783,9 @@ __shared__ uint32_t sr_lds_pid[SR_WG];
 struct HitLog {
     PS ps;
     int n;
-    __device__ __forceinline__ size_t id() const { return (size_t)sr_lds_pid[threadIdx.x]; }
+    // a volatile read where it is used: the hit-record address is not hoisted
+    // out of the step loop (a 64-bit VGPR pair there was spilled)
+    __device__ __forceinline__ size_t id() const { return (size_t)*(volatile const uint32_t*)&sr_lds_pid[threadIdx.x]; }
 };
 
 // Chord end point of step j, frag:924: (nv cos phi_j + tv sin phi_j) / u_j
@@ -1802,7 +1888,7 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 // sr_wave_costs: budget events of each wave of the integrate kernel's workgroup
 __shared__ int sr_lds_ev[SR_WG / 64];
 
-template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET>
+template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
@@ -1811,7 +1897,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     bs.E = lds_E + threadIdx.x;
     bs.pa0 = SR_E_PA0;
     bs.slab0 = SR_E_SLAB0;
-    bs.uhi = INFINITY;
+    if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                     fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
@@ -1887,12 +1973,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 // displacement from the old centre to the chord start r.ro
                 // here, the new chord at the forced event (reseeded)
                 if (CULL)
-                    bs.T = __builtin_fmaf(len(r.ro - (r.nv * bs.cx + r.tv * bs.cy)), 1.0101f,
-                                          3.0e-6f * (fabsf(bs.cx) + fabsf(bs.cy) + 1.0f));
+                {
+                    const float ocx = bs.cx(), ocy = bs.cy();
+                    bs.setT(__builtin_fmaf(len(r.ro - (r.nv * ocx + r.tv * ocy)), 1.0101f,
+                                           3.0e-6f * (fabsf(ocx) + fabsf(ocy) + 1.0f)));
+                }
 #endif
-                f3 q;
-                if (!sphere_test(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius, -1.0f, q))
+                float lam;
+                if (!sphere_lambda_r2(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius2, -1.0f, lam))
                     return flat_misses(sc, r.ro, r.rd) ? ST_BG : ST_FLAT;
+                const f3 q = r.ro + r.rd * lam;  // sphere_intersect's point (computed past the exit)
                 r.nv = nrm(q);
                 if (fabsf(dot(r.rd, r.nv)) >= 1.0f - SR_EPS) return flat_misses(sc, r.ro, r.rd) ? ST_BG : ST_FLAT;
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
@@ -1911,16 +2001,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // forced), an exit (u < 0) or a reseed at the next step (u < u_f).
         // Only numbers leave the loop (lane-mask booleans carried out of it
         // cost exec-mask bookkeeping on every step).
-        const float lim0 = (every || force) ? -INFINITY : bs.m;
-        const float ulo = bs.ulo(fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
+        const float bm = bs.m();
+        const float lim0 = (every || force) ? -INFINITY : bm;
+        const float uhi = bs.uhi();  // u > uhi: the chord left the black hole's u window
+        const float ulo = Budget::ulo_of(uhi, fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
 #if SR_BALL
-        const float bn = CULL ? -2.0f * bs.cx : 0.0f, bt = CULL ? -2.0f * bs.cy : 0.0f;
-        const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bs.m, bs.cx, bs.cy);
+        const float bcx = CULL ? bs.cx() : 0.0f, bcy = CULL ? bs.cy() : 0.0f;
+        const float bn = -2.0f * bcx, bt = -2.0f * bcy;
+        const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bm, bcx, bcy);
         float vb;  // the step's ball test (< 0: inside)
 #endif
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
         // (bs.cm changes only at reseeds, outside the fast loop)
-        const bool any_cm = CULL && __ballot(bs.cm != 0u);
+        const uint32_t bcm = CULL ? bs.cm() : 0u;
+        const bool any_cm = CULL && __ballot(bcm != 0u);
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
         const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
@@ -1939,7 +2033,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs cd = CM ? cyl_dirs(sc, bs) : CylDirs{};
 #if SR_BALL
-            const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bs.m, bs.mh), bs.cx, bs.cy)) : q0;
+            const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bm, bs.mh()), bcx, bcy)) : q0;
 #endif
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
@@ -1954,16 +2048,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 float q = q0;
                 if (CULL && CM) {
                     rB = __builtin_amdgcn_rcpf(un);
-                    par = chord_parallel(bs.cm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
+                    par = chord_parallel(bcm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
                     q = par ? qh : q0;
                 }
                 vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
-                return __ballot(!(vb < 0.0f) || un < ulo || un > bs.uhi);
+                return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
 #endif
                 rB = __builtin_amdgcn_rcpf(un);
-                Tn = bs.T;
+                Tn = bs.T();
                 if (CULL) {
                     // chord length bound: sqrt(dr^2 + rA rB g) K_i, K_i covering the 1e-4
                     // relative allowance, point_err (<= 4e-6 (2 / sqrt(g) + 1) sqrt(...):
@@ -1973,19 +2067,19 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
                     Tn = __builtin_fmaf(sq, e1.z, Tn);
                     if (CM) {
-                        par = chord_parallel(bs.cm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
-                        lim = par ? nmin(lim0, bs.mh) : lim0;
+                        par = chord_parallel(bcm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
+                        lim = par ? nmin(lim0, bs.mh()) : lim0;
                     }
                 }
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
                 // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord);
                 // un > uhi: the chord left the black hole's u window
-                return __ballot(!(Tn < lim) || un < fr.u_f || un > bs.uhi);
+                return __ballot(!(Tn < lim) || un < fr.u_f || un > uhi);
             };
             // apply step i and move to entry (en, en1) of step i + 1
             auto apply = [&](float4 en, float4 en1) -> bool {
-                if (!SR_BALL) bs.T = Tn;
+                if (!SR_BALL) bs.setT(Tn);
                 up = r.u;
                 r.u = un;
                 r.du = dun;
@@ -1996,24 +2090,24 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 e1 = en1;
                 return ++i >= N;
             };
-            // SR_FAST_UNROLL steps per iteration: the entries of steps i + 1
-            // .. i + SR_FAST_UNROLL are loaded together at its top (the table
+            // FU (SR_FAST_UNROLL) steps per iteration: the entries of steps i + 1
+            // .. i + FU are loaded together at its top (the table
             // holds max_steps + 4 entries), so step i + 1 waits only for loads
             // issued a step earlier, and the copies rename the registers one
             // step would rotate. A use on each exit path keeps the loads where
             // they are issued (sunk to their first use, they would be waited
             // at once).
             for (;;) {
-                float4 nx[2 * SR_FAST_UNROLL];
+                float4 nx[2 * FU];
 #pragma unroll
-                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
+                for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
-                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
+                for (int k = 0; k < FU && !leave; k++) {
                     if (compute()) {
 #pragma unroll
-                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
                         leave = apply(nx[2 * k], nx[2 * k + 1]);
@@ -2034,20 +2128,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             e = ldc(tp);
             float4 e1 = ldc(tp + 1);
             for (;;) {
-                float4 nx[2 * SR_FAST_UNROLL];
+                float4 nx[2 * FU];
 #pragma unroll
-                for (int k = 0; k < 2 * SR_FAST_UNROLL; k++) nx[k] = ldc(tp + 2 + k);
+                for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
-                for (int k = 0; k < SR_FAST_UNROLL && !leave; k++) {
+                for (int k = 0; k < FU && !leave; k++) {
                     rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
                     SR_STAT(0, 1);
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
-                    if (__ballot(un < ulo || un > bs.uhi)) {
+                    if (__ballot(un < ulo || un > uhi)) {
 #pragma unroll
-                        for (int j = 2 * k; j < 2 * SR_FAST_UNROLL; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
                         up = r.u;
@@ -2064,7 +2158,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // the state the full loop leaves: step i's radius, no charge (every budget is +inf)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
-            Tn = bs.T;
+            Tn = bs.T();
             lim = lim0;
             par = 0;
 #if SR_BALL
@@ -2087,7 +2181,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return ST_BG;
         }
         // the chord left the black hole's u window (or the inner one outward)
-        const bool bhx = un > bs.uhi || (un < SR_BH_ULO2 && bs.uhi == SR_BH_U2);
+        const bool bhx = un > uhi || (un < SR_BH_ULO2 && uhi == SR_BH_U2);
 #if SR_BALL
         const bool event = !(vb < 0.0f) || bhx;
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
@@ -2099,8 +2193,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // slots about to run out re-anchor at this event too (within SR_AHEAD
         // of this chord's length plus SR_AHEAD_T of the path since the last
         // event): fewer events, each re-anchoring more
-        const float ahead = SR_AHEAD * (Tn - bs.T) + SR_AHEAD_T * Tn;
-        bs.T = Tn;
+        const float ahead = SR_AHEAD * (Tn - bs.T()) + SR_AHEAD_T * Tn;
+        bs.setT(Tn);
 #endif
         up = r.u;
         r.u = un;
@@ -2132,21 +2226,23 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     const float cx = rB * e.z, cy = rB * e.w;  // Bp = nv cx + tv cy (point_near)
                     const f3 dv = Bp - Ap;
                     const float cl = __builtin_amdgcn_sqrtf(dot(dv, dv));
+                    float T;
                     if (reseeded) {
-                        bs.T += (cl * 1.0001f + pe) * SR_PATH_SLACK;
+                        T = bs.T() + (cl * 1.0001f + pe) * SR_PATH_SLACK;
                     } else {
-                        const float dx = cx - bs.cx, dy = cy - bs.cy;
-                        bs.T = __builtin_fmaf(__builtin_amdgcn_sqrtf(dx * dx + dy * dy), 1.0101f,
-                                              3.0e-6f * (rB + fabsf(bs.cx) + fabsf(bs.cy)));
+                        const float ocx = bs.cx(), ocy = bs.cy();
+                        const float dx = cx - ocx, dy = cy - ocy;
+                        T = __builtin_fmaf(__builtin_amdgcn_sqrtf(dx * dx + dy * dy), 1.0101f,
+                                           3.0e-6f * (rB + fabsf(ocx) + fabsf(ocy)));
                     }
-                    ahead = SR_AHEAD * SR_PATH_SLACK * cl + SR_AHEAD_T * bs.T;
-                    bs.cx = cx;
-                    bs.cy = cy;
+                    bs.setT(T);
+                    ahead = SR_AHEAD * SR_PATH_SLACK * cl + SR_AHEAD_T * T;
+                    bs.setC(cx, cy);
                 }
 #else
                 if (reseeded) {  // new frame: the step's bound used the old radius; charge the chord itself
                     const f3 dv = Bp - Ap;
-                    bs.T += (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK;
+                    bs.setT(bs.T() + (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK);
                 }
 #endif
                 SR_STAT(1, 1);
@@ -2168,7 +2264,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                         SR_STAT(49, __popcll(__ballot(event && !(q0 < INFINITY))));
                         SR_STAT(50, nl);
                         SR_STAT(51, __popcll(__ballot(event && reseeded)));
-                        SR_STAT(52, __popcll(__ballot(event && bs.m < 0.05f)));
+                        SR_STAT(52, __popcll(__ballot(event && bs.m() < 0.05f)));
                         SR_STAT(53, any_cm);
                         {  // the slot holding the smallest budget of each triggering lane
                             int jm = 0;
@@ -2191,7 +2287,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_PT(2);
 #ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
                 {
-                    const bool h0 = !(bs.T < bs.E[0]);
+                    const bool h0 = !(bs.T() < bs.E[0]);
                     const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
                     SR_STAT(23, __popcll(__ballot(h0 && r.u > 1.0f)));
                     SR_STAT(24, __popcll(__ballot(h0 && r.u <= 1.0f && r.u > 0.9f)));
@@ -2211,7 +2307,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     bool any = false;
 #pragma unroll
                     for (int j = 1; j <= 6; j++) {
-                        const bool h = !(bs.T < bs.E[j * SR_E_STRIDE]);
+                        const bool h = !(bs.T() < bs.E[j * SR_E_STRIDE]);
                         any |= h;
                         if (j == 3 || j == 5) {  // the default scene's accretion disk and rectangle
                             const int b = j == 3 ? 23 : 26;
@@ -2347,7 +2443,7 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // NB: budget slots the event path handles (>= the scene's sc->num_budget;
 // sr_launch_geodesic picks SR_NB_SMALL when it suffices: the default scene
 // has six, and phase 1 of an event runs over every slot of the capacity).
-template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET>
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL>
 __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
@@ -2377,6 +2473,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #endif
 #ifdef SR_STATS
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c_start = __builtin_amdgcn_s_memtime();  // shader clock: the in-kernel clock (rec[15])
     unsigned long long evmat = 0;
     int rcv[SR_MAX_BUDGET + 1] = {};
 #endif
@@ -2405,7 +2502,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
-        if (st < 0) st = integrate<CULL, true, WCOST, NB>(sc, segs, tbl, fr, tx, r, hit, log);
+        if (st < 0) st = integrate<CULL, true, WCOST, NB, FU>(sc, segs, tbl, fr, tx, r, hit, log);
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
@@ -2452,6 +2549,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
             for (int j = 0; j <= SR_MAX_BUDGET; j++) rec[4 + j] = (unsigned long long)rcm[j];
             rec[13] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
             rec[14] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (wave, SIMD, CU, SE)
+            rec[15] = __builtin_amdgcn_s_memtime() - c_start;     // shader-clock cycles of the wave
         }
     }
 #endif
@@ -2691,6 +2789,9 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (cull && fr->num_budget <= SR_NB_SMALL && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, 2>), dim3(slots * B * SR_WG_PER_TILE),
+                           dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (cull && fr->num_budget <= SR_NB_SMALL)
         hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);

@@ -89,6 +89,7 @@ struct sr_ctx {
     hipStream_t upload = nullptr;
     // split tiles (sr_set_split): 0 = off
     int split_tiles = 0, split_log2 = 4, split_min_steps = 1;
+    int fast_unroll = 3;  // sr_set_latency_mode: 2
     const int* last_order = nullptr;  // the launch codes of the context's last frame (its next frame's order)
     size_t last_slots = 0;
     // the stream of the context's last launch: a context is used from one
@@ -621,6 +622,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.res_y = (float)height;
     fr.u_f = p->u_f;
     fr.uf_radius = 1.0f / p->u_f;
+    fr.uf_radius2 = fr.uf_radius * fr.uf_radius;  // binary32, as the kernel would compute it
     fr.percent_black = p->percent_black;
     fr.curved_percentage = p->curved_percentage;
     fr.max_steps = p->max_steps;
@@ -643,6 +645,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.split_tiles = ctx->split_tiles;
     fr.split_log2 = ctx->split_log2;
     fr.split_min_steps = ctx->split_min_steps;
+    fr.fast_unroll = ctx->fast_unroll;
     return SR_OK;
 }
 
@@ -1105,6 +1108,12 @@ int sr_set_split(sr_ctx* c, int max_tiles, int lanes_per_wave, int min_steps) {
     c->split_tiles = max_tiles;
     c->split_log2 = lg;
     c->split_min_steps = min_steps;
+    return SR_OK;
+}
+
+int sr_set_latency_mode(sr_ctx* c, int on) {
+    if (!c) return SR_E_INVALID;
+    c->fast_unroll = on ? 2 : 3;
     return SR_OK;
 }
 

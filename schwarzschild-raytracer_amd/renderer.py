@@ -53,6 +53,10 @@ class Renderer:
         abi.check(self.lib.sr_set_split(self.ctx, int(max_tiles), int(lanes_per_wave), int(min_steps)), "sr_set_split")
 
     # ---- rendering -------------------------------------------------------------
+    def set_latency_mode(self, on: bool) -> None:
+        """sr_set_latency_mode: a 2-step fast loop for one frame at a time (pixels unchanged)."""
+        abi.check(self.lib.sr_set_latency_mode(self.ctx, 1 if on else 0), "sr_set_latency_mode")
+
     def set_timing(self, capacity: int) -> None:
         """Record per-kernel HIP events for the next `capacity` frames (0: off)."""
         abi.check(self.lib.sr_debug_set_timing(self.ctx, int(capacity)), "sr_debug_set_timing")

@@ -54,8 +54,8 @@ def main():
     for path in args.libs:
         lib = C.CDLL(str(Path(path).resolve()), mode=C.RTLD_LOCAL)
         for name, (res, argt) in {**abi.SIGNATURES, **abi.EXTRA_SIGNATURES}.items():
-            if name in abi.EXTRA_SIGNATURES and not hasattr(lib, name):
-                continue  # older variants predate some debug exports
+            if not hasattr(lib, name):
+                continue  # older variants predate some exports
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = res, argt
         ctx = C.c_void_p()
