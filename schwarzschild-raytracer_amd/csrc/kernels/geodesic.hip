@@ -23,6 +23,11 @@ __device__ __forceinline__ float4 ldc(const sr_cfloat4* p) {
     const sr_v4f v = *p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
+// the compact step table (SR_CTABLE): 5 floats per step, dword aligned
+typedef float sr_v8f_a4 __attribute__((ext_vector_type(8), aligned(4)));
+typedef float sr_v16f_a4 __attribute__((ext_vector_type(16), aligned(4)));
+typedef const __attribute__((address_space(4))) sr_v8f_a4 sr_cf8a;
+typedef const __attribute__((address_space(4))) sr_v16f_a4 sr_cf16a;
 
 #include "../device_scene.h"
 
@@ -592,6 +597,17 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #define SR_E_STRIDE SR_WG
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
+#endif
+// The fast loop's step table (SR_CTABLE): 5 floats per step {step_size,
+// step_size / 6, cos phi, sin phi, 0.5 step_size}, after the main table's
+// 2 (max_steps + 4) float4 (sr_api.cpp ensure_table), so that one iteration's
+// three entries are a single 16-dword scalar load (15 used) instead of six
+// float4 (24 SGPRs): 8 fewer SGPRs live through the fast loop
+#ifndef SR_CTABLE
+#define SR_CTABLE 1
+#endif
+#if SR_CTABLE && !SR_BALL
+#error "SR_CTABLE drops the entries (g, K) only the SR_BALL = 0 step bound reads"
 #endif
 #ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries);
                         // the latency mode's instantiation runs 2 (sr_set_latency_mode)
@@ -1784,8 +1800,13 @@ struct HitLog {
     PS ps;
     int n;
     // a volatile read where it is used: the hit-record address is not hoisted
-    // out of the step loop (a 64-bit VGPR pair there was spilled)
-    __device__ __forceinline__ size_t id() const { return (size_t)*(volatile const uint32_t*)&sr_lds_pid[threadIdx.x]; }
+    // out of the step loop (a 64-bit VGPR pair there was spilled), through an
+    // LDS-typed pointer: a ds_read with a 32-bit address (a generic pointer is
+    // a flat load with a 64-bit one, also spilled)
+    __device__ __forceinline__ size_t id() const {
+        typedef volatile const __attribute__((address_space(3))) uint32_t lds_u32;
+        return (size_t)*(lds_u32*)&sr_lds_pid[threadIdx.x];
+    }
 };
 
 // Chord end point of step j, frag:924: (nv cos phi_j + tv sin phi_j) / u_j
@@ -2018,6 +2039,15 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
         const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
+#if SR_CTABLE
+        const float* fp = reinterpret_cast<const float*>(tbl + 2 * (N + 4)) + 5 * i;  // compact entry of step i
+        // entry of step i from the compact table: (e, e1) with e1.y = 0.5 step_size
+        auto ldcompact = [&](float4& ee, float4& ee1) {
+            const sr_v8f_a4 v = *(const sr_cf8a*)fp;
+            ee = make_float4(v[0], v[1], v[2], v[3]);
+            ee1 = make_float4(0.0f, v[4], 0.0f, 0.0f);
+        };
+#endif
         float4 e;
         float un, dun, rB, Tn, lim;
         uint32_t par;
@@ -2028,8 +2058,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             constexpr bool CM = decltype(cm_tag)::value;
             lim = lim0;
             par = 0;
+            float4 e1;
+#if SR_CTABLE
+            ldcompact(e, e1);
+#else
             e = ldc(tp);
-            float4 e1 = ldc(tp + 1);
+            e1 = ldc(tp + 1);
+#endif
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs cd = CM ? cyl_dirs(sc, bs) : CylDirs{};
 #if SR_BALL
@@ -2084,7 +2119,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.u = un;
                 r.du = dun;
                 if (!SR_BALL || CM) rA = rB;
+#if SR_CTABLE
+                fp += 5;
+#else
                 tp += 2;
+#endif
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
                 e1 = en1;
@@ -2098,21 +2137,42 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // they are issued (sunk to their first use, they would be waited
             // at once).
             for (;;) {
+#if SR_CTABLE
+                static_assert(FU <= 3, "one 16-dword load holds three compact entries");
+                const sr_v16f_a4 nv = *(const sr_cf16a*)(fp + 5);  // steps i + 1 .. i + 3
+#else
                 float4 nx[2 * FU];
 #pragma unroll
                 for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     if (compute()) {
+#if SR_CTABLE
+                        asm volatile("; keep %0" ::"s"(nv[5 * FU - 1]));
+#else
 #pragma unroll
                         for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+#endif
                         leave = true;
                     } else {
+#if SR_CTABLE
+                        leave = apply(make_float4(nv[5 * k], nv[5 * k + 1], nv[5 * k + 2], nv[5 * k + 3]),
+                                      make_float4(0.0f, nv[5 * k + 4], 0.0f, 0.0f));
+#else
                         leave = apply(nx[2 * k], nx[2 * k + 1]);
+#endif
                     }
                 }
+#if SR_CTABLE
+                // the load's unused dwords: without a use the compiler reuses
+                // their registers while the load is in flight, which waits
+                // for the load at the top of the iteration
+#pragma unroll
+                for (int j = 5 * FU; j < 16; j++) asm volatile("; keep %0" ::"s"(nv[j]));
+#endif
                 if (leave) break;
             }
         };
@@ -2125,12 +2185,21 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // the iterates are the same. Only outward lanes (u < 0.6 falling)
         // coast: u stays finite.
         auto coast = [&]() {
+            float4 e1;
+#if SR_CTABLE
+            ldcompact(e, e1);
+#else
             e = ldc(tp);
-            float4 e1 = ldc(tp + 1);
+            e1 = ldc(tp + 1);
+#endif
             for (;;) {
+#if SR_CTABLE
+                const sr_v16f_a4 nv = *(const sr_cf16a*)(fp + 5);  // steps i + 1 .. i + 3
+#else
                 float4 nx[2 * FU];
 #pragma unroll
                 for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
@@ -2140,19 +2209,33 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
                     if (__ballot(un < ulo || un > uhi)) {
+#if SR_CTABLE
+                        asm volatile("; keep %0" ::"s"(nv[5 * FU - 1]));
+#else
 #pragma unroll
                         for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+#endif
                         leave = true;
                     } else {
                         up = r.u;
                         r.u = un;
                         r.du = dun;
+#if SR_CTABLE
+                        fp += 5;
+                        e = make_float4(nv[5 * k], nv[5 * k + 1], nv[5 * k + 2], nv[5 * k + 3]);
+                        e1 = make_float4(0.0f, nv[5 * k + 4], 0.0f, 0.0f);
+#else
                         tp += 2;
                         e = nx[2 * k];
                         e1 = nx[2 * k + 1];
+#endif
                         leave = ++i >= N;
                     }
                 }
+#if SR_CTABLE
+#pragma unroll
+                for (int j = 5 * FU; j < 16; j++) asm volatile("; keep %0" ::"s"(nv[j]));  // as in fast()
+#endif
                 if (leave) break;
             }
             // the state the full loop leaves: step i's radius, no charge (every budget is +inf)

@@ -361,7 +361,13 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const 
     // + 1) sqrt((r2 - r1)^2 + r1 r2 g) (min(r1, r2) <= sqrt(r1 r2)), so
     // K = (1.0001 + 4.01e-6 (2.001 / sqrt(g) + 1)) x path slack 1.01, rounded
     // up, covers both. Four padding entries (the step loop loads up to four steps ahead).
-    std::vector<float4> h(2 * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
+    // Then the fast loop's compact table (geodesic.hip SR_CTABLE): 5 floats
+    // per step {step_size, step_size / 6, cos phi, sin phi, 0.5 step_size},
+    // the same values, plus padding for a 16-dword load three steps ahead
+    const size_t main4 = 2 * ((size_t)max_steps + 4);
+    const size_t compact4 = (5 * ((size_t)max_steps + 4) + 3) / 4 + 1;
+    std::vector<float4> h(main4 + compact4, make_float4(0.f, 0.f, 0.f, 0.f));
+    float* ct = reinterpret_cast<float*>(h.data() + main4);
     float phi = 0.0f;
     double c1 = 1.0, s1 = 0.0;
     for (int i = 0; i < max_steps; i++) {
@@ -374,6 +380,12 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const 
         g = g > 0.0 ? g * (1.0 + 1e-6) + 1e-30 : 1e-30;  // rounded up
         const double K = (1.0001 + 4.01e-6 * (2.001 / std::sqrt(g) + 1.0)) * 1.01 * (1.0 + 1e-6);
         h[2 * (size_t)i + 1] = make_float4((float)g, 0.5f * step, std::nextafter((float)K, INFINITY), 0.f);
+        float* q = ct + 5 * (size_t)i;
+        q[0] = step;
+        q[1] = step / 6.0f;
+        q[2] = c;
+        q[3] = sn;
+        q[4] = 0.5f * step;
         c1 = c;
         s1 = sn;
     }

@@ -221,6 +221,39 @@ def test_split_tiles_bit_identical(pkg, gpu, lanes):
     assert np.array_equal(ref[:rows], got.cpu().numpy()[:rows])
 
 
+def test_latency_mode_bit_identical(pkg, gpu):
+    """sr_set_latency_mode (the integrate kernel's 2-step fast-loop
+    instantiation) changes how many steps one fast-loop iteration runs, never
+    a pixel: float FragColor, RGBA8 and step counts equal the default
+    kernel's (which the other tests hold to the oracle), alone and with split
+    tiles."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    gpu.set_scene(sc.scene_default(textured=True))
+    gpu.set_test_ray(abi.default_test_ray())
+    params = abi.default_params(max_steps=2000, percent_black=-1.0)
+
+    def frame(cam, W, H):
+        f, b, s = gpu.render_debug(cam, params, W, H)
+        torch.cuda.synchronize()
+        return f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()
+
+    for cam, W, H in ((abi.default_camera(), 480, 270), (sc.random_camera(11), 320, 200)):
+        gpu.set_latency_mode(False)
+        ref = frame(cam, W, H)
+        gpu.set_latency_mode(True)
+        got = frame(cam, W, H)
+        gpu.set_split(24, 16, 1)
+        frame(cam, W, H)  # learns the costs
+        got_split = frame(cam, W, H)
+        gpu.set_split(0)
+        gpu.set_latency_mode(False)
+        for a, b_, c_, what in zip(ref, got, got_split, ("float", "rgba8", "steps")):
+            assert np.array_equal(a, b_), f"{what} differs in latency mode ({W}x{H})"
+            assert np.array_equal(a, c_), f"{what} differs in latency mode with split tiles ({W}x{H})"
+
+
 @pytest.mark.parametrize("split,mode", [(0, 0), (12, 0), (0, 2)])
 def test_batch_equals_single_frames(pkg, gpu, split, mode):
     """sr_render_blocks_batch: B frames with different cameras (the flyby) in

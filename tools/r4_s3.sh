@@ -7,9 +7,9 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4s3; mkdir -p $OUT
 V=schwarzschild-raytracer_amd/lib/variants
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 500 python tools/ab_variants.py $V/libsr_r3.so $V/libsr_lds2.so $V/libsr_xp.so $V/libsr_xp_u2.so --throughput --rounds 4 > $OUT/ab_tp.log 2>&1 || { tail -20 $OUT/ab_tp.log; exit 1; }
+timeout -k 10 500 python tools/ab_variants.py $V/libsr_r3.so $V/libsr_xp.so $V/libsr_xp_u2.so $V/libsr_ct.so --throughput --rounds 4 > $OUT/ab_tp.log 2>&1 || { tail -20 $OUT/ab_tp.log; exit 1; }
 grep -E '"lib|median_ms_per_frame|identical' $OUT/ab_tp.log | tail -8
-timeout -k 10 300 python tools/ab_variants.py $V/libsr_r3.so $V/libsr_lds2.so $V/libsr_xp.so $V/libsr_xp_u2.so --rounds 4 > $OUT/ab_single.log 2>&1 || { tail -20 $OUT/ab_single.log; exit 1; }
+timeout -k 10 300 python tools/ab_variants.py $V/libsr_r3.so $V/libsr_xp.so $V/libsr_xp_u2.so $V/libsr_ct.so --rounds 4 > $OUT/ab_single.log 2>&1 || { tail -20 $OUT/ab_single.log; exit 1; }
 grep -E '"lib|median_ms"|identical' $OUT/ab_single.log | tail -8
 timeout -k 10 200 python tools/stats_frame.py $V/libsr_stats.so > $OUT/stats.json 2>&1 || exit 1
 timeout -k 10 200 python tools/stats_frame.py $V/libsr_stats_noxp.so > $OUT/stats_noxp.json 2>&1 || exit 1
