@@ -106,7 +106,8 @@ def kernel_sha() -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=96,
+                    help="timed frames (96: twelve 8-frame launches, the pipeline in steady state rather than one fill)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="headline",
                     help="BASELINE.json config (width x height / steps); --width/--height/--max-steps override")

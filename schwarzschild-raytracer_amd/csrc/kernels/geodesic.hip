@@ -1724,7 +1724,17 @@ struct PS {
     }
     __device__ __forceinline__ float4 get_rec(size_t id) const { return *reinterpret_cast<const float4*>(p + 4 * id); }
     __device__ __forceinline__ float* hit(size_t id, int j) const {
-        return p + 4 * n + ((size_t)j * n + id) * 8;
+        float* const row = p + 4 * n + (size_t)j * n * 8;  // hit j's plane
+        return row + id * 8;
+    }
+    // the same for a 32-bit id (the integrate kernel's LDS pixel ids): one
+    // 32 x 32 + 64-bit multiply-add, no zero-extended id (the compiler kept
+    // that zero in a register spilled across the step loop)
+    __device__ __forceinline__ float* hit32(uint32_t id, int j) const {
+        const uint64_t row = reinterpret_cast<uint64_t>(p + 4 * n + (size_t)j * n * 8);
+        uint64_t a, carry;
+        asm("v_mad_u64_u32 %0, %1, %2, 32, %3" : "=v"(a), "=s"(carry) : "v"(id), "v"(row));
+        return reinterpret_cast<float*>(a);
     }
     // planes of the resumable / flat-ray state
     __device__ __forceinline__ float& at(int f, size_t id) const { return p[(size_t)(PS_PLANES + f) * n + id]; }
@@ -1802,10 +1812,14 @@ struct HitLog {
     // a volatile read where it is used: the hit-record address is not hoisted
     // out of the step loop (a 64-bit VGPR pair there was spilled), through an
     // LDS-typed pointer: a ds_read with a 32-bit address (a generic pointer is
-    // a flat load with a 64-bit one, also spilled)
-    __device__ __forceinline__ size_t id() const {
+    // a flat load with a 64-bit one, also spilled); the index passes through
+    // an empty asm so that the LDS address is formed here too (hoisted, it was
+    // one more register live across the step loop, spilled)
+    __device__ __forceinline__ uint32_t id() const {
         typedef volatile const __attribute__((address_space(3))) uint32_t lds_u32;
-        return (size_t)*(lds_u32*)&sr_lds_pid[threadIdx.x];
+        uint32_t t = threadIdx.x;
+        asm volatile("" : "+v"(t));
+        return *(lds_u32*)&sr_lds_pid[t];
     }
 };
 
@@ -2438,11 +2452,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 // r.steps: the ray's step count if this hit ends it
                 // the whole 32-byte sector in two 16-byte stores (a partial
                 // sector costs a read-modify-write)
-                float4* h = reinterpret_cast<float4*>(log.ps.hit(log.id(), log.n));
+                float4* h = reinterpret_cast<float4*>(log.ps.hit32(log.id(), log.n));
                 h[0] = make_float4(hit.p.x, hit.p.y, hit.p.z,
                                    __int_as_float((int)((uint32_t)(hit.slot * 8 + hit.face + PS_KEY_BIAS) |
                                                                   ((uint32_t)r.steps << 8))));
-                h[1] = make_float4(r.rd.x, r.rd.y, r.rd.z, 0.0f);
+                h[1] = make_float4(r.rd.x, r.rd.y, r.rd.z, hit.p.x);  // .w unread (a zero here was a spilled register)
                 log.n++;
                 if (op == OP_OPAQUE) return ST_HIT;
                 if (log.n == SR_PS_HITS) return ST_MORE;
