@@ -598,13 +598,18 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
-// The fast loop's step table (SR_CTABLE): 5 floats per step {step_size,
-// step_size / 6, cos phi, sin phi, 0.5 step_size}, after the main table's
-// 2 (max_steps + 4) float4 (sr_api.cpp ensure_table), so that one iteration's
-// three entries are a single 16-dword scalar load (15 used) instead of six
-// float4 (24 SGPRs): 8 fewer SGPRs live through the fast loop
+// The fast loop's compact step table (SR_CTABLE = 1): 5 floats per step
+// {step_size, step_size / 6, cos phi, sin phi, 0.5 step_size}, after the main
+// table's 2 (max_steps + 4) float4 (sr_api.cpp ensure_table), so that one
+// iteration's three entries are a single 16-dword scalar load (15 used)
+// instead of six float4 (24 SGPRs). 8 fewer SGPRs live through the fast loop
+// and no VGPR spills in the hot instantiation, but the compiler then rotates
+// u, u' and the previous u through extra moves (44 VALU per step instead of
+// 42.3) and the pipeline renders 7.4 % fewer frames per second (0.972 vs
+// 0.903 ms per frame, interleaved, profiles/r04/s4_ab_tp.log and
+// s5_ab_tp.log; one frame alone 1.4 % sooner). Off: the headline is throughput.
 #ifndef SR_CTABLE
-#define SR_CTABLE 1
+#define SR_CTABLE 0
 #endif
 #if SR_CTABLE && !SR_BALL
 #error "SR_CTABLE drops the entries (g, K) only the SR_BALL = 0 step bound reads"

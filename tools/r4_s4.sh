@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/r4s4; mkdir -p $OUT
 V=schwarzschild-raytracer_amd/lib/variants
-L="$V/libsr_r3.so $V/libsr_xp.so $V/libsr_ct0.so $V/libsr_noxp.so schwarzschild-raytracer_amd/lib/libsr.so"
+L="$V/libsr_xp.so $V/libsr_ct0.so $V/libsr_noxp.so schwarzschild-raytracer_amd/lib/libsr.so"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -3 $OUT/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python tools/ab_variants.py $L --throughput --rounds 4 > $OUT/ab_tp.log 2>&1 || { tail -20 $OUT/ab_tp.log; exit 1; }
 grep -E '"lib|median_ms_per_frame|identical' $OUT/ab_tp.log | tail -10
