@@ -38,6 +38,6 @@ python tools/traffic_json.py --frame "$OUT/p3" "$OUT/p4" --out "$OUT/traffic_lat
 cp "$OUT/pmc_latest.json" "$OUT/traffic_latest.json" /tmp/
 step stats 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --pmc-json /tmp/pmc_latest.json --traffic-json /tmp/traffic_latest.json --critical-path off ${BENCH_ARGS:-}
 grep '^{' "$OUT/stats.log" > "$OUT/bench_stats.json" || true
-python tools/trace_kernel_ms.py "$OUT/prof" --warmup 4 --steps 20 --bench-json "$OUT/bench_stats.json" > "$OUT/kernel_ms_agreement.json" 2>&1
+python tools/trace_kernel_ms.py "$OUT/prof" --warmup 3 --steps ${STATS_STEPS:-96} --bench-json "$OUT/bench_stats.json" > "$OUT/kernel_ms_agreement.json" 2>&1
 cat "$OUT/kernel_ms_agreement.json"
 echo "session done"
