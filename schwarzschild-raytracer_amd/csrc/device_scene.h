@@ -195,6 +195,9 @@ typedef struct {
     // the scene's budget slots (sr_dev_scene.num_budget): picks the integrate
     // kernel's slot capacity (geodesic.hip SR_NB_SMALL)
     int32_t num_budget;
+    // the scene's budgeted cylinders (popcount of sr_dev_scene.budget_cyl_mask;
+    // the small instantiation handles SR_NC_SMALL)
+    int32_t num_budget_cyl;
     // sqrt(8 (1 - out_dip)), rounded up: at least the step angle (the budget
     // events' directional plane window, geodesic.hip plane_window)
     float max_dphi;

@@ -624,19 +624,22 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #ifndef SR_COAST  // the RK4-only fast loop of waves whose every budget is +inf (integrate)
 #define SR_COAST 1
 #endif
-#define SR_E_PA0 (SR_MAX_BUDGET + 1)                      // pa[k] = E[(SR_E_PA0 + 2k) * stride], pb[k] next
-#define SR_E_SLAB0 (SR_MAX_BUDGET + 1 + 2 * SR_MAX_CYLINDERS)  // H[k], slab budgets of the budgeted cylinders
-// the budget's per-lane scalars (Budget::T() ... cm()): not needed inside
-// the fast loop, so they wait in LDS instead of registers (held in VGPRs
-// across it they were spilled to scratch and reloaded at every event)
-#define SR_E_BT (SR_MAX_BUDGET + 1 + 3 * SR_MAX_CYLINDERS)
-#define SR_E_BM (SR_E_BT + 1)
-#define SR_E_BCX (SR_E_BT + 2)
-#define SR_E_BCY (SR_E_BT + 3)
-#define SR_E_BMH (SR_E_BT + 4)
-#define SR_E_BCM (SR_E_BT + 5)
-#define SR_E_BUHI (SR_E_BT + 6)
-#define SR_E_ROWS (SR_E_BT + 7)
+// The budget state's LDS rows (one column per thread) for an
+// instantiation with NB budget slots and NC budgeted cylinders: E[0..NB],
+// then pa[k], pb[k] (rows PA0 + 2k, + 1) and the slab budgets H[k] (SLAB0 +
+// k) of the cylinders, then the budget's per-lane scalars (Budget::T() ...
+// uhi()), which the fast loop does not need, so they wait in LDS instead of
+// registers (held in VGPRs across it they were spilled to scratch and
+// reloaded at every event). The default scene's kernel (6 slots, 1 cylinder)
+// takes 17 rows, 4.25 KiB per 64-lane wave.
+template <int NB, int NC>
+struct BudgetLayout {
+    static constexpr int PA0 = NB + 1;
+    static constexpr int SLAB0 = PA0 + 2 * NC;
+    static constexpr int BT = SLAB0 + NC;
+    static constexpr int BM = BT + 1, BCX = BT + 2, BCY = BT + 3, BMH = BT + 4, BCM = BT + 5, BUHI = BT + 6;
+    static constexpr int ROWS = BT + 7;
+};
 // The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
 // the step's angle dphi at the origin, so it stays in the half-plane beyond
@@ -707,42 +710,44 @@ __device__ __forceinline__ float ball_q(float R, float cx, float cy) {
     return __builtin_fmaf(2.0e-6f * s, s, (cx * cx + cy * cy) - Rt * Rt);
 }
 
+template <int NB_, int NC_>
 struct Budget {
+    using L = BudgetLayout<NB_, NC_>;
+    static constexpr int NB = NB_, NC = NC_;
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
-    int pa0, slab0;  // LDS rows of pa[0] and H[0] (SR_E_PA0 / SR_E_SLAB0)
-    // Scalars in LDS rows (SR_E_BT ..), read with volatile loads so that no
+    // Scalars in LDS rows (L::BT ..), read with volatile loads so that no
     // register holds them across the fast loop:
     //   T   the charge since the last event (slacked path; SR_BALL: displacement)
     //   m   min_j E[j]
     //   cx, cy  SR_BALL: the ball's centre, the last event's end point in the orbital plane (nv, tv)
-    //   mh  min_k of the cylinders' slab budgets H[k] (E[slab0 + k]): the bound
+    //   mh  min_k of the cylinders' slab budgets H[k] (E[SLAB0 + k]): the bound
     //       that covers chords nearly parallel to an axis
     //   cm  budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
     //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; SR_BH_U2:
     //       the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo_of())
     __device__ __forceinline__ float ld(int row) const { return E[row * SR_E_STRIDE]; }
     __device__ __forceinline__ void st(int row, float v) const { E[row * SR_E_STRIDE] = v; }
-    __device__ __forceinline__ float T() const { return ld(SR_E_BT); }
-    __device__ __forceinline__ void setT(float v) const { st(SR_E_BT, v); }
-    __device__ __forceinline__ float m() const { return ld(SR_E_BM); }
-    __device__ __forceinline__ void setM(float v) const { st(SR_E_BM, v); }
-    __device__ __forceinline__ float cx() const { return ld(SR_E_BCX); }
-    __device__ __forceinline__ float cy() const { return ld(SR_E_BCY); }
+    __device__ __forceinline__ float T() const { return ld(L::BT); }
+    __device__ __forceinline__ void setT(float v) const { st(L::BT, v); }
+    __device__ __forceinline__ float m() const { return ld(L::BM); }
+    __device__ __forceinline__ void setM(float v) const { st(L::BM, v); }
+    __device__ __forceinline__ float cx() const { return ld(L::BCX); }
+    __device__ __forceinline__ float cy() const { return ld(L::BCY); }
     __device__ __forceinline__ void setC(float x, float y) const {
-        st(SR_E_BCX, x);
-        st(SR_E_BCY, y);
+        st(L::BCX, x);
+        st(L::BCY, y);
     }
-    __device__ __forceinline__ float mh() const { return ld(SR_E_BMH); }
-    __device__ __forceinline__ void setMh(float v) const { st(SR_E_BMH, v); }
-    // the SR_E_BCM row holds cm in bits 0..7 and the orbit's excluded slots
+    __device__ __forceinline__ float mh() const { return ld(L::BMH); }
+    __device__ __forceinline__ void setMh(float v) const { st(L::BMH, v); }
+    // the L::BCM row holds cm in bits 0..7 and the orbit's excluded slots
     // (bit 8 + j: slot j, budget_frame) above
-    __device__ __forceinline__ uint32_t cm() const { return __float_as_uint(ld(SR_E_BCM)) & 0xffu; }
-    __device__ __forceinline__ uint32_t excl() const { return __float_as_uint(ld(SR_E_BCM)) >> 8; }
+    __device__ __forceinline__ uint32_t cm() const { return __float_as_uint(ld(L::BCM)) & 0xffu; }
+    __device__ __forceinline__ uint32_t excl() const { return __float_as_uint(ld(L::BCM)) >> 8; }
     __device__ __forceinline__ void setCm(uint32_t cm, uint32_t excl) const {
-        st(SR_E_BCM, __uint_as_float(cm | (excl << 8)));
+        st(L::BCM, __uint_as_float(cm | (excl << 8)));
     }
-    __device__ __forceinline__ float uhi() const { return ld(SR_E_BUHI); }
-    __device__ __forceinline__ void setUhi(float v) const { st(SR_E_BUHI, v); }
+    __device__ __forceinline__ float uhi() const { return ld(L::BUHI); }
+    __device__ __forceinline__ void setUhi(float v) const { st(L::BUHI, v); }
     static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
@@ -759,16 +764,17 @@ struct Budget {
 // a rounding allowance far above the frame's non-orthonormality) no chord of
 // this orbit can be near-parallel to the axis and bit k of bs.cm stays clear:
 // chord_parallel skips the cylinder for this lane.
-__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 nv, f3 tv) {
+template <class BS>
+__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
     uint32_t cm = 0;
 #pragma unroll
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+    for (int k = 0; k < BS::NC; k++) {
         if (c) {
             const f3 ax = ld3(sc->slots[__builtin_ctz(c)].a1);
             const float pa = dot(nv, ax), pb = dot(tv, ax);
-            bs.E[(bs.pa0 + 2 * k) * SR_E_STRIDE] = pa;
-            bs.E[(bs.pa0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
+            bs.E[(BS::L::PA0 + 2 * k) * SR_E_STRIDE] = pa;
+            bs.E[(BS::L::PA0 + 1 + 2 * k) * SR_E_STRIDE] = pb;
             // NaN frames keep the test (the comparison is false)
             cm |= (uint32_t)(!(pa * pa + pb * pb < 1.0f - 2.0f * SR_BUDGET_DPMIN - 1.0e-3f)) << k;
             c &= c - 1;
@@ -807,13 +813,15 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
 }
 
 // bs.cm's bit for slot j (budgeted cylinders; false for other slots)
-__device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc, const Budget& bs, int j) {
+template <class BS>
+__device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc, const BS& bs, int j) {
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;
     if (!((cyl >> (j - 1)) & 1u)) return false;
     return (bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
 }
 
-__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 nv, f3 tv,
+template <class BS>
+__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
@@ -859,10 +867,10 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     float mh = INFINITY;
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
 #pragma unroll
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+    for (int k = 0; k < BS::NC; k++) {
         if (c) {
             const float e = clearance_slab(sc->slots[__builtin_ctz(c)], A, a) - m0;
-            bs.E[(bs.slab0 + k) * SR_E_STRIDE] = e;
+            bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE] = e;
             mh = nmin(mh, e);
             c &= c - 1;
         }
@@ -872,18 +880,20 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 
 // The orbit's (pa, pb) on each budgeted cylinder's axis (budget_frame),
 // read from LDS once per fast loop: they change only at reseeds.
+template <int NC>
 struct CylDirs {
-    float pa[SR_MAX_CYLINDERS], pb[SR_MAX_CYLINDERS];
+    float pa[NC], pb[NC];
 };
-__device__ __forceinline__ CylDirs cyl_dirs(const sr_dev_scene* __restrict__ sc, const Budget& bs) {
-    CylDirs d;
+template <class BS>
+__device__ __forceinline__ CylDirs<BS::NC> cyl_dirs(const sr_dev_scene* __restrict__ sc, const BS& bs) {
+    CylDirs<BS::NC> d;
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
 #pragma unroll
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+    for (int k = 0; k < BS::NC; k++) {
         d.pa[k] = d.pb[k] = 0.0f;
         if (c) {
-            d.pa[k] = bs.E[(bs.pa0 + 2 * k) * SR_E_STRIDE];
-            d.pb[k] = bs.E[(bs.pa0 + 1 + 2 * k) * SR_E_STRIDE];
+            d.pa[k] = bs.E[(BS::L::PA0 + 2 * k) * SR_E_STRIDE];
+            d.pb[k] = bs.E[(BS::L::PA0 + 1 + 2 * k) * SR_E_STRIDE];
             c &= c - 1;
         }
     }
@@ -896,12 +906,13 @@ __device__ __forceinline__ CylDirs cyl_dirs(const sr_dev_scene* __restrict__ sc,
 // budget_cyl_mask). Decided with twice the threshold and forced when the
 // direction is not known to 0.4%. Branch-free over the cylinder capacity
 // (unused slots have pa = pb = 0 and no bit in cm).
-__device__ __forceinline__ uint32_t chord_parallel(uint32_t cm, const CylDirs& cd, float a, float b, float perr) {
+template <int NC>
+__device__ __forceinline__ uint32_t chord_parallel(uint32_t cm, const CylDirs<NC>& cd, float a, float b, float perr) {
     const float dd = a * a + b * b;
     const bool vague = !(perr * perr <= 1.6e-5f * dd);
     uint32_t par = 0;
 #pragma unroll
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+    for (int k = 0; k < NC; k++) {
         const float ca = a * cd.pa[k] + b * cd.pb[k];
         const bool near = vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd);
         par |= (uint32_t)near << k;
@@ -1001,25 +1012,26 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // slot capacity, no per-slot branches or LDS round trips), then only the
 // slots some lane has spent - usually one - run their clearance and reach
 // tests; all lanes re-anchor those.
-template <int NB>
-__device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, Budget& bs, f3 A, f3 B,
+template <class BS>
+__device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
                                                  bool falling) {
+    constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
     const float T = bs.T();
-    float e[NS], h[SR_MAX_CYLINDERS];
+    float e[NS], h[NC];
 #pragma unroll
     for (int j = 0; j < NS; j++) e[j] = bs.E[j * SR_E_STRIDE];
     {
         uint32_t c = cyl;  // only the scene's cylinders' rows exist in the packed layout
 #pragma unroll
-        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        for (int k = 0; k < NC; k++) {
             h[k] = INFINITY;
             if (c) {
-                h[k] = bs.E[(bs.slab0 + k) * SR_E_STRIDE];
+                h[k] = bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE];
                 c &= c - 1;
             }
         }
@@ -1030,7 +1042,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     {
         uint32_t c = cyl;
 #pragma unroll
-        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        for (int k = 0; k < NC; k++) {
             if (c) {
                 const bool f = reanchor_cyl || (((par >> k) & 1u) && !(T < h[k]));
                 forced |= (uint32_t)f << (__builtin_ctz(c) + 1);
@@ -1076,11 +1088,11 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     {
         uint32_t c = cyl;
 #pragma unroll
-        for (int k = 0; k < SR_MAX_CYLINDERS; k++) {
+        for (int k = 0; k < NC; k++) {
             if (c) {
                 if (!((spent >> (__builtin_ctz(c) + 1)) & 1u)) {
                     const float v = h[k] - T;
-                    bs.E[(bs.slab0 + k) * SR_E_STRIDE] = v;
+                    bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE] = v;
                     mh = nmin(mh, v);
                 }
                 c &= c - 1;
@@ -1147,7 +1159,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (TY == SR_OBJECT_CYLINDER) {
                 const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
                 const float vh = clearance_slab(st, B, a) - perr;
-                bs.E[(bs.slab0 + k) * SR_E_STRIDE] = vh;
+                bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE] = vh;
                 mh = nmin(mh, vh);
             }
             if (__ballot(h) && __ballot(h && slot_reachable(&st, j, A, B, perr))) reach |= 1u << j;
@@ -1928,15 +1940,15 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 // sr_wave_costs: budget events of each wave of the integrate kernel's workgroup
 __shared__ int sr_lds_ev[SR_WG / 64];
 
-template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL>
+template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL,
+          int NC = SR_MAX_CYLINDERS>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
-    __shared__ float lds_E[SR_E_ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
-    Budget bs;
+    using BS = Budget<NB, NC>;
+    __shared__ float lds_E[BS::L::ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
+    BS bs;
     bs.E = lds_E + threadIdx.x;
-    bs.pa0 = SR_E_PA0;
-    bs.slab0 = SR_E_SLAB0;
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
@@ -1945,7 +1957,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     bs.fires = 0;
     struct Out {
         Ray& r;
-        Budget& b;
+        BS& b;
         __device__ ~Out() { r.steps = b.fires; }
     } out_{r, bs};
 #endif
@@ -2044,7 +2056,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const float bm = bs.m();
         const float lim0 = (every || force) ? -INFINITY : bm;
         const float uhi = bs.uhi();  // u > uhi: the chord left the black hole's u window
-        const float ulo = Budget::ulo_of(uhi, fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
+        const float ulo = BS::ulo_of(uhi, fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
 #if SR_BALL
         const float bcx = CULL ? bs.cx() : 0.0f, bcy = CULL ? bs.cy() : 0.0f;
         const float bn = -2.0f * bcx, bt = -2.0f * bcy;
@@ -2085,7 +2097,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             e1 = ldc(tp + 1);
 #endif
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
-            const CylDirs cd = CM ? cyl_dirs(sc, bs) : CylDirs{};
+            const CylDirs<NC> cd = CM ? cyl_dirs(sc, bs) : CylDirs<NC>{};
 #if SR_BALL
             const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bm, bs.mh()), bcx, bcy)) : q0;
 #endif
@@ -2423,7 +2435,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
-                reach = budget_event<NB>(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                          fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
                 SR_PT(6);
 #ifdef SR_STATS
@@ -2510,6 +2522,12 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #ifndef SR_NB_SMALL
 #define SR_NB_SMALL 6
 #endif
+// budgeted cylinders of the small instantiation: its cylinder loops (phase 1,
+// chord_parallel in the cylinder-plane fast loop) run over one, and its LDS
+// layout holds 17 rows instead of 25 (no VGPR spills left in it)
+#ifndef SR_NC_SMALL
+#define SR_NC_SMALL 1
+#endif
 
 // Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
 // tile << 8 | SR_SPLIT | sub for workgroup `sub` of a split tile; -1 for an
@@ -2545,7 +2563,8 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // NB: budget slots the event path handles (>= the scene's sc->num_budget;
 // sr_launch_geodesic picks SR_NB_SMALL when it suffices: the default scene
 // has six, and phase 1 of an event runs over every slot of the capacity).
-template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL>
+// NC: budgeted cylinders it handles (SR_NC_SMALL with SR_NB_SMALL).
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS>
 __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
@@ -2604,7 +2623,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
 #endif
-        if (st < 0) st = integrate<CULL, true, WCOST, NB, FU>(sc, segs, tbl, fr, tx, r, hit, log);
+        if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
@@ -2696,7 +2715,12 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 // split workgroups each (their waves carry a few rays: a wave's budget events
 // are the union of its lanes', so the longest rays run with fewer events);
 // the grid's remaining slots get -1. Resets the costs. One workgroup.
-__global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, int n, int max_cost,
+// One 256-thread workgroup (a wave per SIMD): with 1024 threads it needed
+// sixteen wave slots on one CU, which the integrate launches of the other
+// streams rarely left free, and its stream waited up to 6.5 ms behind it
+// (mean 0.35 ms per launch, profiles/r04/s6_kernel_stats.csv).
+#define SR_ORDER_WG 256
+__global__ __launch_bounds__(SR_ORDER_WG) void sr_order_kernel(int* __restrict__ cost, int n, int max_cost,
                                                         int* __restrict__ order, int split_tiles, int split_log2,
                                                         int split_min) {
     __shared__ int hist[256];
@@ -2718,7 +2742,7 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
     };
     if (t < 256) hist[t] = 0;
     __syncthreads();
-    for (int i = t; i < n; i += 1024) atomicAdd(&hist[bucket(cost[i])], 1);
+    for (int i = t; i < n; i += SR_ORDER_WG) atomicAdd(&hist[bucket(cost[i])], 1);
     __syncthreads();
     if (t == 0) {
         int run = 0, hi = 0;
@@ -2732,7 +2756,7 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
     __syncthreads();
     const int S = 64 >> split_log2;  // split workgroups per tile
     const int ns = nsplit;
-    for (int i = t; i < n; i += 1024) {
+    for (int i = t; i < n; i += SR_ORDER_WG) {
         const int p = atomicAdd(&offs[bucket(cost[i])], 1);
         if (p < ns) {
             for (int sub = 0; sub < S; sub++) order[p * S + sub] = (i << 8) | SR_SPLIT | sub;
@@ -2741,7 +2765,7 @@ __global__ __launch_bounds__(1024) void sr_order_kernel(int* __restrict__ cost, 
         }
         cost[i] = 0;
     }
-    for (int j = n + (S - 1) * ns + t; j < n + (S - 1) * split_tiles; j += 1024) order[j] = -1;
+    for (int j = n + (S - 1) * ns + t; j < n + (S - 1) * split_tiles; j += SR_ORDER_WG) order[j] = -1;
 }
 
 __global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __restrict__ sc,
@@ -2887,15 +2911,18 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (nblocks > (1u << 22)) return hipErrorInvalidValue;  // tile << 8 stays a positive int
     const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
+    // the small instantiation (6 slots, 1 cylinder: 17 LDS rows) when the scene fits it
+    const bool small = cull && fr->num_budget <= SR_NB_SMALL && fr->num_budget_cyl <= SR_NC_SMALL;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
-    else if (cull && fr->num_budget <= SR_NB_SMALL && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
-        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, 2>), dim3(slots * B * SR_WG_PER_TILE),
+    else if (small && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, 2, SR_NC_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
-    else if (cull && fr->num_budget <= SR_NB_SMALL)
-        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
+    else if (small)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, SR_FAST_UNROLL, SR_NC_SMALL>),
+                           dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (cull)
         hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
@@ -2915,7 +2942,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
         hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     if (order)
-        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(1024), 0, stream, cost, (int)nblocks, fr->max_steps, order,
+        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(SR_ORDER_WG), 0, stream, cost, (int)nblocks, fr->max_steps, order,
                            split, split ? fr->split_log2 : 6, fr->split_min_steps);
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();

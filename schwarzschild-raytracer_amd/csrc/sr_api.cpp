@@ -678,6 +678,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.batch = n_frames;
     // the black hole's u window (geodesic.hip SR_BH_WINDOW): chord origins within r = 100
     fr.num_budget = ctx->h_scene.num_budget;
+    fr.num_budget_cyl = __builtin_popcount((unsigned)ctx->h_scene.budget_cyl_mask);
     fr.win_ok = fr.uf_radius <= 100.0f;
     for (int f = 0; f < n_frames; f++) {
         const float* q = fr.cam[f].pos;

@@ -4,7 +4,8 @@ K:LANES:MIN_STEPS (K = 0: off) and each share of the headline frame, the
 single-frame latency (one context alone) and the time per frame with F frames
 in flight (F contexts on their own streams), frames byte-compared with the
 unsplit render.
-  python tools/split_sweep.py --split 0:16:1 64:16:1000 ... [--shard 0 1 --shard 0 8] [--inflight 4]
+  python tools/split_sweep.py --split 0:16:1 64:16:1000 64:16:1000:L ... [--shard 0 1 --shard 0 8] [--inflight 4]
+(a fourth field L: with the latency mode, sr_set_latency_mode)
 Prints one JSON line per (setting, share)."""
 import argparse
 import json
@@ -84,9 +85,12 @@ def main():
                 cs = [cams[(f * Bt + j) % nf] for j in range(n)]
                 rs[k].render_blocks_batch(cs, params, W, H, 8, rank, world, out=outs[k][:n], stream=ss[k])
 
-        K, lanes, mn = (int(x) for x in spec.split(":"))
+        fields = spec.split(":")
+        K, lanes, mn = (int(x) for x in fields[:3])
+        latency_mode = len(fields) > 3 and fields[3] == "L"  # K:LANES:MIN:L = with sr_set_latency_mode
         for r in rs:
             r.set_split(K, lanes, mn)
+            r.set_latency_mode(latency_mode)
         for k in range(Fmax):  # learn each context's launch order (twice: split codes need costs)
             for f in range(3):
                 go(k, f)
