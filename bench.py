@@ -157,7 +157,7 @@ def parse():
                     help="rows of the frame swept on the CPU for `value` (0 = every row: the full frame)")
     ap.add_argument("--single-frame", choices=["on", "off"], default="on",
                     help="also time single-frame launches (N = 1): one frame alone, and 4 in flight")
-    ap.add_argument("--single-split", default="64:16:1000",
+    ap.add_argument("--single-split", default="32:16:1200",
                     help="split tiles for the latency figure of one frame alone: max_tiles[:lanes[:min_steps]] "
                          "(0 = off; the costliest tiles' rays in sparse waves, DESIGN.md §6)")
     ap.add_argument("--dump-frames", default="",
@@ -651,16 +651,20 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
             times.append(e0.elapsed_time(e1))
         return statistics.median(times)
 
-    # the latency mode (sr_set_latency_mode: 2-step fast loop) with split tiles,
-    # then the default kernel without them
-    for rk, _, _ in pool:
-        rk.set_latency_mode(True)
+    # split tiles (the frame's costliest tiles' rays in sparse waves), then
+    # the default launch, then the latency mode (sr_set_latency_mode: a 2-step
+    # fast loop) without split tiles (with them it measured slower: s8)
     learn(split)
     alone = one_alone()
+    learn((0, 16, 1))
+    alone_unsplit = one_alone()
+    for rk, _, _ in pool:
+        rk.set_latency_mode(True)
+    learn((0, 16, 1))
+    alone_latency = one_alone()
     for rk, _, _ in pool:
         rk.set_latency_mode(False)
     learn((0, 16, 1))
-    alone_unsplit = one_alone()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for j in range(frames):
@@ -678,9 +682,12 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
     return {
         "alone": {"frames_per_launch": 1, "launches_in_flight": 1, "ms_per_frame": round(alone, 4),
                   "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events",
-                  "split_tiles": split_arg, "latency_mode": True},
+                  "split_tiles": split_arg, "latency_mode": False},
         "alone_default": {"ms_per_frame": round(alone_unsplit, 4), "mpix_s": round(W * H / alone_unsplit / 1e3, 3),
                           "split_tiles": "0", "latency_mode": False},
+        "alone_latency_mode": {"ms_per_frame": round(alone_latency, 4),
+                               "mpix_s": round(W * H / alone_latency / 1e3, 3), "split_tiles": "0",
+                               "latency_mode": True},
         "inflight": {"frames_per_launch": 1, "launches_in_flight": inflight, "ms_per_frame": round(per, 4),
                      "mpix_s": round(W * H / per / 1e3, 3), "frames": frames, "stat": "wall clock",
                      "split_tiles": "0"},

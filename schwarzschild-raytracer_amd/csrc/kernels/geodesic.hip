@@ -2768,7 +2768,10 @@ __global__ __launch_bounds__(SR_ORDER_WG) void sr_order_kernel(int* __restrict__
     for (int j = n + (S - 1) * ns + t; j < n + (S - 1) * split_tiles; j += SR_ORDER_WG) order[j] = -1;
 }
 
-__global__ __launch_bounds__(256) void sr_shade_kernel(const sr_dev_scene* __restrict__ sc,
+#ifndef SR_SHADE_WAVES_PER_EU
+#define SR_SHADE_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(256, SR_SHADE_WAVES_PER_EU) void sr_shade_kernel(const sr_dev_scene* __restrict__ sc,
                                                       const float* __restrict__ segs,
                                                       const uint32_t* __restrict__ bg,
                                                       const uint32_t* __restrict__ arr, sr_dev_frame fr,
