@@ -554,6 +554,56 @@ __device__ __forceinline__ sr_dev_slot pin_slot(const sr_dev_slot& g) {
     return sl;
 }
 
+// Plane window of a budgeted cylinder (SR_CYL_PLANE, round 4): a budget
+// from the orbital plane instead of the distance to the cylinder. Every chord
+// of the orbit lies within 1e-6 r + 1e-4 of the plane span(nv, tv) through the
+// origin (its binary32 end points, as budget_frame's exclusion), so it passes
+// at least hx - that from the bounding centre bc, hx = |bc . n| / |n|. When no
+// chord of the orbit can be nearly parallel to the axis (bs.cm's bit clear:
+// |d_perp|^2 >= 2 SR_BUDGET_DPMIN), may_hit lets a chord reach the cylinder
+// only within br + mu S + qk (S + |pos|_1)^2 of bc (qk = SR_CYL_QMARGIN /
+// (r SR_BUDGET_DPMIN) covers the quadratic's root error with a factor 2 to
+// spare; mu the quadratic factor, above the planar one may_hit uses), S = |o|_1
+// + len + 1. So chords with S <= S_max, the largest S at which that reach is
+// below hx less the rounding, cannot be hit; the chords in a ball of radius W
+// around the anchor C have S <= |C|_1 + (2 + sqrt 3) W + 1 (origins within W
+// of C, lengths within 2 W): the budget is the W for S_max. It replaces the
+// distance budget when larger (lanes passing the cylinder off its plane:
+// 90 % of the cylinder's re-anchors, profiles/r04/s11_stats_xcyl.json).
+// Returns 0 when the plane is too near (or the frame NaN). Measured
+// (profiles/r04/s12_*, frames bit-identical): the cylinder's re-anchors 124.5 k
+// -> 49.6 k per headline frame, but events 339.6 k -> 345.3 k (the events the
+// cylinder no longer triggers re-anchored other slots ahead of their own
+// expiry) and the frame time unchanged (0.848 vs 0.849 ms); off.
+#ifndef SR_CYL_PLANE
+#define SR_CYL_PLANE 0
+#endif
+// SR_QPLANE: the same window for spheres and boxes (no quadratic term: their
+// reach is br + mu S in every direction, mu their own factor); planes far
+// enough from them are excluded outright (budget_frame). Measured with the
+// cylinder's (s12): sphere re-anchors 21.8 k -> 16.5 k, events 345.3 k ->
+// 341.7 k, frame time +0.7 %; off.
+#ifndef SR_QPLANE
+#define SR_QPLANE 0
+#endif
+__device__ __forceinline__ float plane_window_x(const sr_dev_slot& sl, f3 nv, f3 tv, f3 C, float mu, float q) {
+    const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
+    const float hx = fabsf(dot(ld3(sl.bc), n)) * __builtin_amdgcn_rsqf(dot(n, n)) * (1.0f - 1.0e-5f);
+    // room for the reach: hx less the chords' distance from the plane (end
+    // points within 1e-6 r + 1e-4 of it, r <= |C| + 3 W <= 3100 for W <= 1000)
+    // and the rounding of hx, then the bounding radius
+    const float room = (hx - (3.2e-3f + 1.0e-5f * sl.cn)) * (1.0f / 1.001f) - sl.br;
+    if (!(room > 0.0f)) return 0.0f;
+    // largest x = S + |pos|_1 with qk x^2 + mu x <= room + mu |pos|_1 (the
+    // positive root in its cancellation-free form)
+    const float c = room + mu * sl.pl1;
+    const float x = 2.0f * c / (mu + __builtin_amdgcn_sqrtf(__builtin_fmaf(4.0f * q, c, mu * mu)));
+    const float smax = (x - sl.pl1) * 0.999f;
+    const float c1 = fabsf(C.x) + fabsf(C.y) + fabsf(C.z);
+    const float w = (smax * (1.0f / 1.001f) - c1 - 1.0f) * (1.0f / 3.7321f) * 0.999f;
+    return w > 0.0f ? fminf(w, 1000.0f) : 0.0f;  // NaN -> 0
+}
+
 // Direction-independent part of a budgeted cylinder's clearance: the distance
 // from A to its height slab (0 <= (p - pos) . axes[1] <= height). cyl_test
 // accepts only a point p = o + lambda d with 0 <= lambda <= len, i.e. on the
@@ -858,6 +908,14 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     for (int j = 1; j <= nb; j++) {
         const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);  // one batch of scalar loads per slot
         float e = clearance_obj(sl, A, a) - m0;
+        if (SR_CYL_PLANE && sl.type == SR_OBJECT_CYLINDER && !cyl_par_bit(sc, bs, j)) {
+            const float w = plane_window_x(sl, nv, tv, A, SR_MU_QUADRATIC, sl.qk) - m0;
+            e = w > e ? w : e;  // a NaN e stays NaN
+        }
+        if (SR_QPLANE && (sl.type == SR_OBJECT_SPHERE || sl.type == SR_OBJECT_BOX)) {
+            const float w = plane_window_x(sl, nv, tv, A, sl.mu, 0.0f) - m0;
+            e = w > e ? w : e;
+        }
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
         bs.E[j * SR_E_STRIDE] = e;
@@ -1016,7 +1074,7 @@ template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
-                                                 bool falling) {
+                                                 bool falling, f3 nv, f3 tv) {
     constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
@@ -1064,6 +1122,14 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (__ballot((forced >> j) & 1u)) spent |= 1u << j;
     }
     spent &= (2u << nb) - 1u;
+#ifdef SR_STATS_XCYL  // measurement only (tools/stats_frame.py --xcyl)
+    uint32_t trig = 0;  // slots some lane has spent itself (not look-ahead)
+#pragma unroll
+    for (int j = 0; j < NS; j++)
+        if (__ballot(!(T < e[j]) || ((forced >> j) & 1u))) trig |= 1u << j;
+    trig &= (2u << nb) - 1u;
+    if (!trig) SR_STAT(53, 1);  // an event no slot's budget asked for (the ball test's margins)
+#endif
     SR_PTB(20);
 #ifdef SR_PROF
     {
@@ -1148,6 +1214,21 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 const float w = plane_window(st, A, B, ao, perr, dphi);
                 v = w > v ? w : v;  // NaN v stays NaN
             }
+            if (SR_CYL_PLANE && TY == SR_OBJECT_CYLINDER &&
+                !((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u)) {
+                // the frame's normal computed here: hoisted out of the slot
+                // loop it was held across it and spilled
+                f3 nv_ = nv, tv_ = tv;
+                asm volatile("" : "+v"(nv_.x), "+v"(nv_.y), "+v"(nv_.z), "+v"(tv_.x), "+v"(tv_.y), "+v"(tv_.z));
+                const float w = plane_window_x(st, nv_, tv_, B, SR_MU_QUADRATIC, st.qk) - perr;
+                v = w > v ? w : v;  // a NaN v stays NaN
+            }
+            if (SR_QPLANE && (TY == SR_OBJECT_SPHERE || TY == SR_OBJECT_BOX)) {
+                f3 nv_ = nv, tv_ = tv;
+                asm volatile("" : "+v"(nv_.x), "+v"(nv_.y), "+v"(nv_.z), "+v"(tv_.x), "+v"(tv_.y), "+v"(tv_.z));
+                const float w = plane_window_x(st, nv_, tv_, B, st.mu, 0.0f) - perr;
+                v = w > v ? w : v;
+            }
             if (TY != SR_OBJECT_PLANE && outward &&
                 outward_slot(st, TY == SR_OBJECT_CYLINDER &&
                                      ((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
@@ -1158,6 +1239,23 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             m = nmin(m, v);
             if (TY == SR_OBJECT_CYLINDER) {
                 const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
+#ifdef SR_STATS_XCYL
+                {  // could an orbital-plane exclusion of the cylinder have avoided this re-anchor?
+                    const f3 nrm_ = cross(A, B);
+                    const float nn = dot(nrm_, nrm_), hd = dot(ld3(st.bc), nrm_);
+                    const bool cmb = (bs.cm() >> k) & 1u;
+                    auto far = [&](float D) { return nn > 1.0e-6f * dot(A, A) * dot(B, B) && hd * hd > D * D * nn; };
+                    SR_STAT(44, 1);
+                    if (!__ballot(h)) SR_STAT(51, 1);
+                    SR_STAT(48, __popcll(__ballot(h)));
+                    SR_STAT(49, __popcll(__ballot(h && cmb)));
+                    SR_STAT(50, __popcll(__ballot(h && !far(3.6f))));
+                    if (!__ballot(h && (cmb || !far(3.6f)))) SR_STAT(45, 1);
+                    if (!__ballot(h && (cmb || !far(5.0f)))) SR_STAT(46, 1);
+                    if (!__ballot(h && (cmb || !far(8.0f)))) SR_STAT(47, 1);
+                    if (trig == (1u << j) && !__ballot(h && (cmb || !far(3.6f)))) SR_STAT(52, 1);
+                }
+#endif
                 const float vh = clearance_slab(st, B, a) - perr;
                 bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE] = vh;
                 mh = nmin(mh, vh);
@@ -2368,7 +2466,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
                     const int nl = __popcll(__ballot(event));
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
-#if SR_BALL
+#if SR_BALL && !defined(SR_STATS_XCYL)  // (SR_STATS_XCYL: counters 44..53 in budget_event instead)
                     if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
                     SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
                     SR_STAT(46, __popcll(__ballot(bhx)));
@@ -2436,7 +2534,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
+                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, r.nv, r.tv);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
