@@ -3035,7 +3035,10 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
                        out, pitch, dbg_rgba, dbg_steps, list, count, diag);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
-    unsigned nb = (nblocks * B < 1024u ? nblocks * B : 1024u) * SR_WG_PER_TILE;
+#ifndef SR_RESUME_TILES  // the resume kernel's grid-stride grid, in 256-thread tiles
+#define SR_RESUME_TILES 1024u
+#endif
+    unsigned nb = (nblocks * B < SR_RESUME_TILES ? nblocks * B : SR_RESUME_TILES) * SR_WG_PER_TILE;
     if (cull)
         hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
