@@ -2064,8 +2064,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     // the test rays are present (wave-uniform)
     const bool every = !CULL || sc->num_step > 0 || sc->tr_visible;
     // Chord bookkeeping: im = the step whose chord r.ro / r.rd hold; up = u
-    // after step i - 2; rA ~ 1 / u after step i - 1. r.steps = sbase + (steps
-    // begun). In sr_integrate_kernel the step index i is wave-uniform.
+    // after step i - 2 (outside the fast loop: it leaves `up` behind and
+    // recover_up() recomputes it); rA ~ 1 / u after step i - 1. r.steps =
+    // sbase + (steps begun). In sr_integrate_kernel the step index i is
+    // wave-uniform.
     int im = r.i - 1;
     float up = 0.0f;
     float rA = __builtin_amdgcn_rcpf(r.u);
@@ -2218,6 +2220,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
+#if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
+                if (CM) SR_STAT(31, 1);  // wave-steps of the cylinder-plane fast loop
+#endif
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
 #endif
                 rB = __builtin_amdgcn_rcpf(un);
@@ -2244,7 +2249,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // apply step i and move to entry (en, en1) of step i + 1
             auto apply = [&](float4 en, float4 en1) -> bool {
                 if (!SR_BALL) bs.setT(Tn);
-                up = r.u;
                 r.u = un;
                 r.du = dun;
                 if (!SR_BALL || CM) rA = rB;
@@ -2346,7 +2350,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
                         leave = true;
                     } else {
-                        up = r.u;
                         r.u = un;
                         r.du = dun;
 #if SR_CTABLE
@@ -2377,11 +2380,33 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             vb = -1.0f;  // inside every (infinite) budget
 #endif
         };
+        // The fast loop does not carry `up` (u after step i - 2): the copy
+        // cost a register move per step in its rotation (42.3 -> 41.7 VALU
+        // per step). The two exits that need it - u < 0 (the previous chord,
+        // frag:921-922) and the end of the loop - recompute it from the
+        // loop's entry state with the same RK4 steps (bit-identical).
+        const int ick = i;
+        const float uck = r.u, duck = r.du, upck = up;
+        auto recover_up = [&](int ie) -> float {  // u after step ie - 2
+            if (ie == ick) return upck;
+            float u = uck, du = duck;
+            for (int j = ick; j < ie - 1; j++) {  // steps ick .. ie - 2
+                const float4 t0 = tbl[2 * j], t1 = tbl[2 * j + 1];
+                float un2, dun2;
+                rk4_step(u, du, t0.x, t1.y, t0.y, un2, dun2);  // the fast loop's operands
+                u = un2;
+                du = dun2;
+            }
+            return u;
+        };
         if (any_cm) fast(std::true_type{});
         else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
         else fast(std::false_type{});
         SR_PT(0);
-        if (i >= N) break;
+        if (i >= N) {
+            up = recover_up(N);
+            break;
+        }
 #ifdef SR_PROF
         if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[19] += 1;
 #endif
@@ -2389,6 +2414,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         r.i = i;
         r.steps = sbase + i + 1;
         if (un < 0.0f) {
+            up = recover_up(i);
             settle_prev(i);
             return ST_BG;
         }

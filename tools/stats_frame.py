@@ -65,6 +65,7 @@ def main():
     out["handoff"] = {"pixels": int(buf[23]), "hit_records": int(buf[24]),
                       **{n: int(buf[25 + k]) for k, n in enumerate(["done", "hit", "more", "flat", "bg", "bh"])}}
     out["event_frac"] = out["events"] / max(1, out["wave_steps"])
+    out["cm_wave_steps"] = int(buf[31])  # plain SR_STATS builds: wave-steps of the cylinder-plane fast loop
     if hasattr(lib, "sr_debug_stats_hi"):  # counters 32..63 of the same frame
         hi = (C.c_ulonglong * 32)()
         lib.sr_debug_stats_hi.restype = C.c_int
