@@ -532,6 +532,27 @@ def test_reseed_headline_rows(pkg, gpu, oracle, oracle_tex, name, pos, fov, u_f)
         assert (rs[0] != s[y]).sum() == 0, f"{name}: row {y} step counts"
 
 
+@pytest.mark.parametrize("max_steps,revs", [(2000, 2), (600, 1)])
+def test_negative_u_exits(pkg, gpu, oracle, oracle_tex, max_steps, revs):
+    """Rays that leave by u < 0 (frag:921-922: get_bg with the previous
+    chord) rather than by the u_f reseed: with u_f = 1e-4 an escaping ray's u
+    steps from above 1e-4 straight below 0, so every escaping lane takes the
+    exit whose previous chord needs u after step i - 2, which the fast loop
+    does not carry (integrate's recover_up replays the RK4 steps). With one
+    revolution of the step schedule (frag:20) over 600 steps, rays near the
+    photon ring also reach the end of the loop (the other replay). Whole
+    320x180 frames, bit-exact with step counts."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.default_camera()
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=1.0e-4, max_revolutions=revs)
+    g = gpu_debug(gpu, scene, cam, params, 320, 180)
+    o = oracle.render(scene, cam, params, 320, 180, oracle_tex)
+    print(compare(g, o, f"u_f 1e-4, {max_steps} steps, {revs} revolutions"))  # pixels, float bits, steps
+    if revs == 1:
+        assert (o[2] == max_steps).sum() > 50  # rays that ran to the end of the loop
+
+
 def test_reference_assets_frame(pkg, oracle):
     """The reference's own textures through the ingest path (assets/textures:
     2k.jpg skybox, uv_checker.jpg + cubemap.png array, image_utils.cpp:7-117)
