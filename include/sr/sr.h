@@ -368,15 +368,18 @@ int sr_render_debug(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, 
  * steps as waves of lanes_per_wave (16, 4 or 1) rays instead of 64. A wave's
  * budget events are the union of its rays' events, so the frame's longest
  * rays finish sooner in sparse waves, at the cost of more waves for those
- * tiles. max_tiles 0 (the default) turns it off. */
+ * tiles. max_tiles 0 (the default) turns it off. For one
+ * headline frame at a time (1920x1080, 2000 steps) sr_set_split(ctx, 32, 16,
+ * 1200) measured 1.148 ms against 1.163 ms without (profiles/r04/s16). */
 int sr_set_split(sr_ctx* ctx, int max_tiles, int lanes_per_wave, int min_steps);
 
 /* Latency mode (not in the reference; the pixels are unchanged): on != 0 runs
  * the next frames' step loop with two fast-loop steps per iteration instead of
- * three: one frame alone finishes ~5 % sooner (its longest rays' dependency
- * chain), frames in flight run ~0.5 % slower. For an interactive caller that
- * draws one frame at a time (src/main.cpp:318-319); pair it with sr_set_split
- * (the costliest tiles' rays in sparse waves). Off by default. */
+ * three: one frame alone finishes sooner (its longest rays' dependency
+ * chain: 1.277 -> 1.128 ms in profiles/r04/s8_split_sweep.jsonl), frames in
+ * flight run ~2 % slower. For an interactive caller that draws one frame at
+ * a time (src/main.cpp:318-319) without split tiles: with them it measured
+ * slower than split tiles alone. Off by default. */
 int sr_set_latency_mode(sr_ctx* ctx, int on);
 
 /* Rows a sr_render_blocks call with these arguments writes. */
