@@ -133,6 +133,7 @@ __device__ const uint8_t* sr_lane_mask;
 //   0 fast loop  1 reseeds  2 slow-path entry + approximate chord  3 budget events phase 1
 //   4 exact chord + intersect  5 hit classification + log  6 budget events phase 2  7 wave total
 #define SR_PROF_N 24  // 0-6 sections, 7 wave total | max steps << 48, 8-15 re-anchors of budget slots 0-7,
+                      // 22 budget_init, 23 kernel start to integrate (launch code, pixel, ray set-up),
                       // 16 budget events, 17 events spending only slot 0, 18 lanes spending slot 0 (sum),
                       // 19 slow-path entries, 20 event phase 1 up to the spent ballots (the rest
                       // in 3), 21 slow-path tail + top of the step loop (2: exit to the event)
@@ -671,6 +672,9 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #ifndef SR_AHEAD_T
 #define SR_AHEAD_T 1.0f
 #endif
+#ifndef SR_CM_ITER  // the cylinder-plane fast loop tests the chord direction once per iteration (integrate)
+#define SR_CM_ITER 1
+#endif
 #ifndef SR_COAST  // the RK4-only fast loop of waves whose every budget is +inf (integrate)
 #define SR_COAST 1
 #endif
@@ -1074,7 +1078,7 @@ template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
-                                                 bool falling, f3 nv, f3 tv) {
+                                                 bool falling, f3 nv, f3 tv, bool par_recompute) {
     constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
@@ -1093,6 +1097,25 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 c &= c - 1;
             }
         }
+    }
+    if (par_recompute) {
+        // the event chord's direction against the budgeted cylinders' axes
+        // (chord_parallel in 3-D on the approximate chord; the fast loop's
+        // CMV 2 tested only its iteration's first chord)
+        par = 0;
+        const f3 dv = B - A;
+        const float dd = dot(dv, dv);
+        const bool vague = !(perr * perr <= 1.6e-5f * dd);
+        uint32_t c = cyl;
+#pragma unroll
+        for (int k = 0; k < NC; k++) {
+            if (c) {
+                const float ca = dot(dv, ld3(sc->slots[__builtin_ctz(c)].a1));
+                par |= (uint32_t)(vague | !(dd - ca * ca >= 2.0f * SR_BUDGET_DPMIN * dd)) << k;
+                c &= c - 1;
+            }
+        }
+        par &= bs.cm();
     }
     // this lane's slots whose E does not cover the chord (bit 0: the chord
     // left the black hole's u window, bhx)
@@ -2047,6 +2070,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     __shared__ float lds_E[BS::L::ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     BS bs;
     bs.E = lds_E + threadIdx.x;
+#ifdef SR_PROF
+    const unsigned prof_bi_ = (unsigned)clock64();  // budget_init's cycles (section 22)
+#endif
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
@@ -2106,6 +2132,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     unsigned prof_t_ = (unsigned)clock64();
     bs.prof = r.prof;
     bs.pt = &prof_t_;
+    if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[22] += prof_t_ - prof_bi_;
 #endif
     for (;;) {
         if (RECORD) i = __builtin_amdgcn_readfirstlane(i);  // every lane started at step 0: keep i scalar
@@ -2182,11 +2209,22 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         float4 e;
         float un, dun, rB, Tn, lim;
         uint32_t par;
-        // Two versions of the loop: without a lane whose orbital plane nearly
-        // contains a budgeted cylinder's axis (the usual case) the limit is
-        // fixed and there is no direction test.
+        // Three versions of the loop: without a lane whose orbital plane nearly
+        // contains a budgeted cylinder's axis (the usual case, CMV 0) the
+        // limit is fixed and there is no direction test; with one, the chord's
+        // direction is tested on every step (CMV 1) or, when every lane is in
+        // a black-hole u window, on the first step of each three-step
+        // iteration only (CMV 2, SR_CM_ITER): with u <= SR_BH_U2 at every
+        // applied step's ends the orbit's tangent turns by at most 1.5 u per
+        // radian of phi (dpsi/dphi = 1.5 u^3 / (u^2 + u'^2)), so the next two
+        // chords lie within 4.53 max_dphi of the tested one's direction, below
+        // the 0.0555 rad between chord_parallel's threshold (|d_perp|^2 <
+        // 2 SR_BUDGET_DPMIN, direction known to 0.004) and the margin's
+        // (|d_perp|^2 >= SR_BUDGET_DPMIN). The exit step's chord is tested
+        // again in the slow path (its end may lie beyond the window).
         auto fast = [&](auto cm_tag) {
-            constexpr bool CM = decltype(cm_tag)::value;
+            constexpr int CMV = decltype(cm_tag)::value;
+            constexpr bool CM = CMV != 0;
             lim = lim0;
             par = 0;
             float4 e1;
@@ -2204,18 +2242,28 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
             if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            float qit = q0;  // CMV 2: the iteration's ball
             // Step i from entry (e, e1): RK4, the chord-length bound and the
             // exit test; true when some lane needs attention (the step is then
-            // computed but not applied).
-            auto compute = [&]() -> bool {
+            // computed but not applied). k: the step's place in the iteration.
+            auto compute = [&](int k) -> bool {
                 rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
 #if SR_BALL
                 // the end point against the ball (ball_q): a multiply and three FMAs
                 float q = q0;
-                if (CULL && CM) {
+                if (CULL && CMV == 1) {
                     rB = __builtin_amdgcn_rcpf(un);
                     par = chord_parallel(bcm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
                     q = par ? qh : q0;
+                }
+                if (CULL && CMV == 2) {
+                    if (k == 0) {
+                        const float ra = __builtin_amdgcn_rcpf(r.u);
+                        rB = __builtin_amdgcn_rcpf(un);
+                        par = chord_parallel(bcm, cd, rB * e.z - ra * pc.x, rB * e.w - ra * pc.y, point_err(ra, rB));
+                        qit = par ? qh : q0;
+                    }
+                    q = qit;
                 }
                 vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
                 SR_STAT(0, 1);
@@ -2251,7 +2299,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (!SR_BALL) bs.setT(Tn);
                 r.u = un;
                 r.du = dun;
-                if (!SR_BALL || CM) rA = rB;
+                if (!SR_BALL || CMV == 1) rA = rB;
 #if SR_CTABLE
                 fp += 5;
 #else
@@ -2282,7 +2330,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
-                    if (compute()) {
+                    if (compute(k)) {
 #if SR_CTABLE
                         asm volatile("; keep %0" ::"s"(nv[5 * FU - 1]));
 #else
@@ -2399,9 +2447,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             }
             return u;
         };
-        if (any_cm) fast(std::true_type{});
+        // CMV 2 needs every lane in a u window (u <= SR_BH_U2 at applied steps)
+        // and the three chords' turning 1.5 SR_BH_U2 x 1.01 x 3 max_dphi within 0.05
+        const bool cm_iter = SR_CM_ITER && any_cm && !__ballot(!(uhi <= SR_BH_U2)) &&
+                             4.53f * fr.max_dphi < 0.05f;
+        if (cm_iter) fast(std::integral_constant<int, 2>{});
+        else if (any_cm) fast(std::integral_constant<int, 1>{});
         else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
-        else fast(std::false_type{});
+        else fast(std::integral_constant<int, 0>{});
         SR_PT(0);
         if (i >= N) {
             up = recover_up(N);
@@ -2560,7 +2613,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, r.nv, r.tv);
+                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, r.nv, r.tv,
+                                         cm_iter);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
@@ -2746,6 +2800,7 @@ __global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kerne
 #endif
 #ifdef SR_PROF
         r.prof = prof_lds[threadIdx.x >> 6];
+        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[23] += (unsigned)(clock64() - prof_t0);
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
         const size_t id = log.id();

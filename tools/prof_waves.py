@@ -63,7 +63,10 @@ def main():
     out["slow_entries_all_waves"] = int(t[ok, 19].sum())
     out["phase1_ballots_all_waves"] = int(t[ok, 20].sum())
     out["tail_top_all_waves"] = int(t[ok, 21].sum())
-    out["unaccounted_cycles_all_waves"] = int(total[ok].sum() - sums.sum() - t[ok, 20].sum() - t[ok, 21].sum())
+    out["budget_init_all_waves"] = int(t[ok, 22].sum())  # builds since round 4 (0 before)
+    out["ray_setup_all_waves"] = int(t[ok, 23].sum())  # kernel start to integrate: launch code, pixel, ray
+    out["unaccounted_cycles_all_waves"] = int(total[ok].sum() - sums.sum() - t[ok, 20].sum() - t[ok, 21].sum()
+                                              - t[ok, 22].sum() - t[ok, 23].sum())
     gx = (1920 + 15) // 16
     top = np.argsort(-total)[: args.top]
     out["slowest"] = [
