@@ -818,8 +818,17 @@ struct Budget {
 // a rounding allowance far above the frame's non-orthonormality) no chord of
 // this orbit can be near-parallel to the axis and bit k of bs.cm stays clear:
 // chord_parallel skips the cylinder for this lane.
+// slot j's orbital-plane exclusion bit (below), n = nv x tv, nn = |n|^2
+__device__ __forceinline__ uint32_t xplane_bit(const sr_dev_slot& sl, int j, f3 n, float nn) {
+    if (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_CYLINDER) return 0u;
+    const float h = dot(ld3(sl.bc), n);  // |h| / |n|: bc's distance from the plane
+    const float need = (sl.br + sl.mu * SR_XPLANE_S) * 1.001f + 1.0e-4f + 1.0e-5f * sl.cn;
+    // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
+    return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
+}
+// the cylinders' (pa, pb) rows and the cm bits (budget_frame, budget_init)
 template <class BS>
-__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
+__device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
     uint32_t cm = 0;
 #pragma unroll
@@ -834,6 +843,11 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
             c &= c - 1;
         }
     }
+    return cm;
+}
+template <class BS>
+__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
+    const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
     uint32_t x = 0;
 #if SR_XPLANE
     // Orbital-plane exclusion (per orbit): every chord of this orbit joins two
@@ -853,14 +867,7 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
         const float nn = dot(n, n);
         const int nb = sc->num_budget;
-        for (int j = 1; j <= nb; j++) {
-            const sr_dev_slot& sl = sc->slots[j - 1];
-            if (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_CYLINDER) continue;
-            const float h = dot(ld3(sl.bc), n);  // |h| / |n|: bc's distance from the plane
-            const float need = (sl.br + sl.mu * SR_XPLANE_S) * 1.001f + 1.0e-4f + 1.0e-5f * sl.cn;
-            // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
-            x |= (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
-        }
+        for (int j = 1; j <= nb; j++) x |= xplane_bit(sc->slots[j - 1], j, n, nn);
     }
 #endif
     bs.setCm(cm, x);
@@ -889,8 +896,12 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     const float m0 = 0.0f;
 #endif
     float m = INFINITY;
-    budget_frame(sc, bs, nv, tv);  // bs.cm first (outward_slot)
-    const uint32_t xcl = bs.excl();
+    // the cm bits first (outward_slot); the exclusion bits in the slot loop
+    const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
+    bs.setCm(cm, 0u);
+    const f3 xn = cross(nv, tv);
+    const float xnn = dot(xn, xn);
+    uint32_t xcl = 0;
     {
         float e = clearance_bh(a);
         float uhi = INFINITY;
@@ -908,9 +919,16 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         bs.E[0] = e;
         m = nmin(m, e);
     }
+    // One pass over the slots; slot j + 1's record is loaded while slot j
+    // is worked on (one batch of scalar loads per slot, waited a slot later:
+    // waited at once they serialised the loop's latency, SR_PROF section 22)
+    sr_dev_slot nxt;
+    if (nb > 0) nxt = sc->slots[0];
 #pragma unroll 1
     for (int j = 1; j <= nb; j++) {
-        const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);  // one batch of scalar loads per slot
+        const sr_dev_slot sl = pin_slot(nxt);
+        if (j < nb) nxt = sc->slots[j];
+        if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn);
         float e = clearance_obj(sl, A, a) - m0;
         if (SR_CYL_PLANE && sl.type == SR_OBJECT_CYLINDER && !cyl_par_bit(sc, bs, j)) {
             const float w = plane_window_x(sl, nv, tv, A, SR_MU_QUADRATIC, sl.qk) - m0;
@@ -925,6 +943,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         bs.E[j * SR_E_STRIDE] = e;
         m = nmin(m, e);
     }
+    bs.setCm(cm, xcl);
     bs.setM(m);
     float mh = INFINITY;
     uint32_t c = (uint32_t)sc->budget_cyl_mask;
