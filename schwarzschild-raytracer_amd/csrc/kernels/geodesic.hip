@@ -686,13 +686,33 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 // registers (held in VGPRs across it they were spilled to scratch and
 // reloaded at every event). The default scene's kernel (6 slots, 1 cylinder)
 // takes 17 rows, 4.25 KiB per 64-lane wave.
+// Side slots (SR_SIDE). A planar slot's distance budget runs out long before
+// most lanes' chords come near the primitive's plane: half of the headline's
+// budget events (168 k of 340 k per frame, profiles/r04/s20) had only planar
+// slots spent, by lanes whose chord stayed off those slots' acceptance slabs
+// (slot_reachable). At such an event the wave instead takes those slots (at
+// most SIDE of them) out of its ball and tests, per step, the side of each
+// slot's plane the chord's end point lies on (side_slots below); the event
+// happens when a chord's end reaches a slab, a non-side budget runs out, or
+// a lane passes the radius the side tests' margins were sized for.
+#ifndef SR_SIDE
+#define SR_SIDE 1
+#endif
+#ifndef SR_SIDE_MAX
+#define SR_SIDE_MAX 1  // side slots per wave (1: the kernel's side_j)
+#endif
 template <int NB, int NC>
 struct BudgetLayout {
     static constexpr int PA0 = NB + 1;
     static constexpr int SLAB0 = PA0 + 2 * NC;
     static constexpr int BT = SLAB0 + NC;
     static constexpr int BM = BT + 1, BCX = BT + 2, BCY = BT + 3, BMH = BT + 4, BCM = BT + 5, BUHI = BT + 6;
-    static constexpr int ROWS = BT + 7;
+    // side slots (SR_SIDE; the small layout only): the ball without them
+    // (QS), the u bound of the side tests' radius (US), and per side slot s
+    // the test's coefficients in rows SP0 + 3 s .. SP0 + 3 s + 2
+    static constexpr int SIDE = (SR_SIDE && NB <= 6 && NC <= 1) ? SR_SIDE_MAX : 0;
+    static constexpr int QS = BT + 7, US = BT + 8, SP0 = BT + 9;
+    static constexpr int ROWS = BT + 7 + (SIDE ? 2 + 3 * SIDE : 0);
 };
 // The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
@@ -801,6 +821,9 @@ struct Budget {
         st(L::BCM, __uint_as_float(cm | (excl << 8)));
     }
     __device__ __forceinline__ float uhi() const { return ld(L::BUHI); }
+    __device__ __forceinline__ float qs() const { return ld(L::QS); }
+    __device__ __forceinline__ float us() const { return ld(L::US); }
+    __device__ __forceinline__ float sp(int s, int k) const { return ld(L::SP0 + 3 * s + k); }
     __device__ __forceinline__ void setUhi(float v) const { st(L::BUHI, v); }
     static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
@@ -1097,7 +1120,8 @@ template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
-                                                 bool falling, f3 nv, f3 tv, bool par_recompute) {
+                                                 bool falling, f3 nv, f3 tv, bool par_recompute,
+                                                 int sj, float sc_, float ss_, float su_) {
     constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
@@ -1137,8 +1161,16 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         par &= bs.cm();
     }
     // this lane's slots whose E does not cover the chord (bit 0: the chord
-    // left the black hole's u window, bhx)
+    // left the black hole's u window, bhx; side slots: their side test)
     uint32_t forced = (uint32_t)bhx;
+    if (BS::L::SIDE > 0 && sj > 0) {
+        // the side slot (side_slots), forced where its side test failed at
+        // this chord's end (cos, sin, u) = (sc_, ss_, su_) or the lane passed
+        // the radius bound (recomputed here: carried from the step loop's
+        // exit, the mask was spilled)
+        const float w = __builtin_fmaf(bs.sp(0, 0), sc_, __builtin_fmaf(bs.sp(0, 1), ss_, -bs.sp(0, 2) * su_));
+        forced |= (uint32_t)(!(w > 0.0f) || su_ < bs.us()) << sj;
+    }
     {
         uint32_t c = cyl;
 #pragma unroll
@@ -1318,6 +1350,91 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     bs.setM(m);
     bs.setMh(mh);
     return reach;
+}
+
+// Side slots (SR_SIDE): at a budget event of the chord [A, B] (exact end
+// points within 4e-6 (rA + rB)) whose lanes have spent only planar slots
+// (mp < inf: the slab test of slot_reachable applies), at most SIDE of them,
+// each lane that spent one with both ends of its chord beyond that slot's
+// slab margin on the same side: the step is applied with no re-anchor and no
+// exact test (the chord cannot reach those slots, and every other budget
+// covers it: T < E[k], the event's own criterion), and the wave goes on with
+// those slots out of each such lane's ball. Per step it then tests the end
+// point X = (c, s) / u against each side slot's plane: y = (alpha c + beta s)
+// / u - g with alpha = nv . a1, beta = tv . a1, g = pos . a1, on the lane's
+// side sg beyond the margin m when sg alpha c + sg beta s - (sg g + m) u > 0.
+// Consecutive end points share their chords, so every chord of the stretch
+// has both ends beyond the slab and slot_reachable's planar test rejects it.
+// m is slot_reachable's margin for chords whose ends lie within Rb = 2.002
+// max(rA, rB) of the origin (S <= (sqrt(3) + 2) Rb + 1 covers |A|_1 + len +
+// 1, perr 8e-6 Rb), plus 1e-5 (Rb + |g| + 1) for the test's own float
+// evaluation (a few eps (2 r + |g| + m) in y) and alpha / beta's rounding;
+// lanes stop at u < 1 / (2 max(rA, rB)) (us). Lanes of the wave that did not
+// need a slot keep its budget in their ball (coefficients 0, 0, -1: always
+// true) unless they too are off its slab. Returns false, with nothing
+// changed, when the event cannot be replaced.
+template <class BS>
+__device__ __forceinline__ bool side_slots(const sr_dev_scene* __restrict__ sc, const BS& bs, f3 A, f3 B, float rA,
+                                           float rB, float cx, float cy, f3 nv, f3 tv, int& side_j) {
+    constexpr int NS = BS::NB + 1;
+    constexpr int SD = BS::L::SIDE;
+    const int nb = sc->num_budget;
+    const float ocx = bs.cx(), ocy = bs.cy();
+    const float dx = cx - ocx, dy = cy - ocy;
+    // the charge the event would make (budget_event: slot j covers the chord when T < E[j])
+    const float T = __builtin_fmaf(__builtin_amdgcn_sqrtf(dx * dx + dy * dy), 1.0101f,
+                                   3.0e-6f * (rB + fabsf(ocx) + fabsf(ocy)));
+    uint32_t sp = 0;  // wave-uniform: slots some lane has spent
+    float mq = INFINITY;  // this lane's ball: every budget but its side slots'
+#pragma unroll
+    for (int j = 0; j < NS; j++) {
+        if (j <= nb) {
+            const float e = bs.E[j * SR_E_STRIDE];
+            if (__ballot(!(T < e))) sp |= 1u << j;
+            else mq = nmin(mq, e);
+        }
+    }
+    if (sp == 0u || (sp & 1u) || __builtin_popcount(sp) > SD) return false;
+    const float Rm = 2.0f * fmaxf(rA, rB);
+    const float Rb = Rm * 1.001f;
+    const float perr = 8.0e-6f * Rb;
+    const float S = __builtin_fmaf(3.7321f, Rb, 1.0f) * 1.001f + perr;
+    int js[SD];
+    bool anyside = false;
+    uint32_t w = sp;
+    const int n = __builtin_popcount(sp);
+#pragma unroll
+    for (int k = 0; k < SD; k++) {
+        js[k] = 0;
+        if (k < n) {
+            const int j = __builtin_ctz(w);
+            w &= w - 1;
+            js[k] = j;
+            const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);
+            if (!(sl.mp < INFINITY) || !(sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_DISK ||
+                                         sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_RECTANGLE))
+                return false;
+            const f3 pos = ld3(sl.pos), a1 = ld3(sl.a1);
+            const float g = dot(pos, a1);
+            const float m = (sl.mp + sl.mu * S) * 1.001f + perr + 1.0e-5f * (Rb + fabsf(g) + 1.0f);
+            const float yA = dot(A - pos, a1), yB = dot(B - pos, a1);
+            const bool side = (yA > m && yB > m) || (yA < -m && yB < -m);
+            const float e = bs.E[j * SR_E_STRIDE];
+            if (__ballot(!(T < e) && !side)) return false;
+            // (rows written before the wave's decision are unread while side_j is 0)
+            const float sg = yB > 0.0f ? 1.0f : -1.0f;
+            bs.st(BS::L::SP0 + 3 * k, side ? sg * dot(nv, a1) : 0.0f);
+            bs.st(BS::L::SP0 + 3 * k + 1, side ? sg * dot(tv, a1) : 0.0f);
+            bs.st(BS::L::SP0 + 3 * k + 2, side ? __builtin_fmaf(sg, g, m) : -1.0f);
+            if (!side) mq = nmin(mq, e);
+            anyside |= side;
+        }
+    }
+    bs.st(BS::L::QS, ball_q(mq, ocx, ocy));
+    bs.st(BS::L::US, anyside ? __builtin_amdgcn_rcpf(Rm) : 0.0f);
+    static_assert(SD == 1, "one side slot (side_j)");
+    side_j = js[0];
+    return true;
 }
 
 // The test rays (frag:760-803), visited right after the black hole.
@@ -2143,6 +2260,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         im = i - 1;
     };
     bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
+    // side slots (SR_SIDE, wave-uniform): how many, and which
+    constexpr bool SIDE = CULL && BS::L::SIDE > 0;
+    int side_j = 0;  // the side slot (side_slots; 0: none - slot 0, the hole, is never one)
     int i = r.i;
 #ifdef SR_STATS
     int last_ev = i;
@@ -2162,6 +2282,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // every reseed happens)
         SR_PT(21);
         if (__ballot(r.u < fr.u_f)) {
+            side_j = 0;  // a new orbital frame: the side tests' coefficients are the old frame's
             if (r.u < fr.u_f) {
                 r.i = i;
                 r.steps = sbase + i + 1;
@@ -2202,11 +2323,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const float bm = bs.m();
         const float lim0 = (every || force) ? -INFINITY : bm;
         const float uhi = bs.uhi();  // u > uhi: the chord left the black hole's u window
-        const float ulo = BS::ulo_of(uhi, fr.u_f);  // u < ulo: a reseed or exit at the next step, or the inner window's end
+        // u < ulo: a reseed or exit at the next step, or the inner window's
+        // end (with a side slot: or the radius bound of its margin)
+        const float ulo = (SIDE && side_j) ? fmaxf(BS::ulo_of(uhi, fr.u_f), bs.us()) : BS::ulo_of(uhi, fr.u_f);
 #if SR_BALL
         const float bcx = CULL ? bs.cx() : 0.0f, bcy = CULL ? bs.cy() : 0.0f;
         const float bn = -2.0f * bcx, bt = -2.0f * bcy;
-        const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bm, bcx, bcy);
+        // (with a side slot: the ball without it, side_slots)
+        const float q0 = (!CULL || every || force) ? INFINITY : (SIDE && side_j) ? bs.qs() : ball_q(bm, bcx, bcy);
         float vb;  // the step's ball test (< 0: inside)
 #endif
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
@@ -2241,9 +2365,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // 2 SR_BUDGET_DPMIN, direction known to 0.004) and the margin's
         // (|d_perp|^2 >= SR_BUDGET_DPMIN). The exit step's chord is tested
         // again in the slow path (its end may lie beyond the window).
-        auto fast = [&](auto cm_tag) {
+        auto fast = [&](auto cm_tag, auto sd_tag) {
             constexpr int CMV = decltype(cm_tag)::value;
             constexpr bool CM = CMV != 0;
+            constexpr int NSD = decltype(sd_tag)::value;  // side slots tested per step (CMV 0 only)
+            static_assert(NSD == 0 || CMV == 0, "side slots with the cylinder-plane loop");
             lim = lim0;
             par = 0;
             float4 e1;
@@ -2260,7 +2386,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
-            if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            // side slots: the ball without them, the lanes' radius bound and
+            // per side slot (sa, sb, sc): the end point (cos phi, sin phi) / u
+            // is off the slot's slab on the lane's side when sa cos phi + sb
+            // sin phi - sc u > 0 (side_slots)
+            float sa[2] = {0.0f, 0.0f}, sb[2] = {0.0f, 0.0f}, scc[2] = {0.0f, 0.0f};
+            if (NSD > 0) {
+#pragma unroll
+                for (int s = 0; s < NSD; s++) {
+                    sa[s] = bs.sp(s, 0);
+                    sb[s] = bs.sp(s, 1);
+                    scc[s] = bs.sp(s, 2);
+                }
+            }
+            if (CM || NSD > 0) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             float qit = q0;  // CMV 2: the iteration's ball
             // Step i from entry (e, e1): RK4, the chord-length bound and the
             // exit test; true when some lane needs attention (the step is then
@@ -2290,6 +2429,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
                 if (CM) SR_STAT(31, 1);  // wave-steps of the cylinder-plane fast loop
 #endif
+#ifdef SR_STATS_PLANE
+                if (NSD > 0) SR_STAT(54, 1);  // wave-steps with side slots
+#endif
+                if (NSD > 0) {
+                    bool sf = false;
+#pragma unroll
+                    for (int s = 0; s < NSD; s++)
+                        sf |= !(__builtin_fmaf(sa[s], e.z, __builtin_fmaf(sb[s], e.w, -scc[s] * un)) > 0.0f);
+                    return __ballot(!(vb < 0.0f) || un < ulo || un > uhi || sf);
+                }
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
 #endif
                 rB = __builtin_amdgcn_rcpf(un);
@@ -2470,10 +2619,21 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // and the three chords' turning 1.5 SR_BH_U2 x 1.01 x 3 max_dphi within 0.05
         const bool cm_iter = SR_CM_ITER && any_cm && !__ballot(!(uhi <= SR_BH_U2)) &&
                              4.53f * fr.max_dphi < 0.05f;
-        if (cm_iter) fast(std::integral_constant<int, 2>{});
-        else if (any_cm) fast(std::integral_constant<int, 1>{});
-        else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
-        else fast(std::integral_constant<int, 0>{});
+        using I0 = std::integral_constant<int, 0>;
+        using I1 = std::integral_constant<int, 1>;
+        using I2 = std::integral_constant<int, 2>;
+        if constexpr (SIDE) {
+            if (side_j) fast(I0{}, I1{});
+            else if (cm_iter) fast(I2{}, I0{});
+            else if (any_cm) fast(I1{}, I0{});
+            else if (SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
+            else fast(I0{}, I0{});
+        } else {
+            if (cm_iter) fast(I2{}, I0{});
+            else if (any_cm) fast(I1{}, I0{});
+            else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
+            else fast(I0{}, I0{});
+        }
         SR_PT(0);
         if (i >= N) {
             up = recover_up(N);
@@ -2493,7 +2653,18 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // the chord left the black hole's u window (or the inner one outward)
         const bool bhx = un > uhi || (un < SR_BH_ULO2 && uhi == SR_BH_U2);
 #if SR_BALL
-        const bool event = !(vb < 0.0f) || bhx;
+        // side slot: lanes whose chord end reached its slab (or passed the
+        // radius its margin was sized for) need an event (budget_event
+        // forces the slot's re-anchor for them)
+        bool sfail = false;
+        if constexpr (SIDE) {
+            static_assert(BS::L::SIDE == 1, "one side slot");
+            if (side_j) {
+                const float w = __builtin_fmaf(bs.sp(0, 0), e.z, __builtin_fmaf(bs.sp(0, 1), e.w, -bs.sp(0, 2) * un));
+                sfail = !(w > 0.0f) || un < bs.us();
+            }
+        }
+        const bool event = !(vb < 0.0f) || bhx || sfail;
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
@@ -2517,12 +2688,30 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             if (!__ballot(event)) break;
             uint32_t reach = 0xffffffffu;
             const f2 p1 = phi_cs(i - 1);
+            int sjx = 0;
             if (CULL) {
                 // the approximate chord (exact start when materialised)
                 const bool exact_start = im == i - 1;
                 const f3 Ap = exact_start ? r.ro : point_near(r, rAold, p1.x, p1.y);
                 const f3 Bp = point_near(r, rB, e.z, e.w);
                 const float pe = point_err(exact_start ? 0.0f : rAold, rB);
+#if SR_BALL
+                if constexpr (SIDE) {
+                    sjx = side_j;  // the side slot this event may force
+                    side_j = 0;
+                    // only planar slots spent, chords off their slabs: no event (side_slots)
+                    if (!every && !any_cm && !__ballot(reseeded || bhx || sfail) &&
+                        side_slots(sc, bs, Ap, Bp, rAold, rB, rB * e.z, rB * e.w, r.nv, r.tv, side_j)) {
+#ifdef SR_STATS_PLANE
+                        SR_STAT(55, 1);
+#endif
+                        break;
+                    }
+#ifdef SR_STATS_PLANE
+                    if (__ballot(sfail)) SR_STAT(57, 1);
+#endif
+                }
+#endif
 #if SR_BALL
                 // the displacement from the ball's centre to the step's end
                 // point Bp, which becomes the centre: bs.T bounds 1.01 x the
@@ -2564,7 +2753,50 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
                     const int nl = __popcll(__ballot(event));
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
-#if SR_BALL && !defined(SR_STATS_XCYL)  // (SR_STATS_XCYL: counters 44..53 in budget_event instead)
+#ifdef SR_STATS_PLANE  // measurement only (tools/stats_frame.py --plane): counters 44..53
+                    {
+                        // a triggering lane is "plane-avoidable" when every slot it has
+                        // spent is planar and this chord stays off that slot's
+                        // acceptance slab (slot_reachable's planar test): a per-step
+                        // plane test would not have stopped it
+                        const float T = bs.T();
+                        const bool trig = event;
+                        bool avoid = trig && !bhx && !reseeded && T < bs.E[0];
+                        bool anyspent = false, anyplanar = false;
+                        const f3 dv = Bp - Ap;
+                        const float ln = __builtin_amdgcn_sqrtf(dot(dv, dv));
+                        const float S = ((fabsf(Ap.x) + fabsf(Ap.y) + fabsf(Ap.z)) + ln + 1.0f) * 1.001f + pe;
+                        for (int j = 1; j <= sc->num_budget && j <= NB; j++) {
+                            if (T < bs.E[j * SR_E_STRIDE]) continue;
+                            anyspent = true;
+                            const sr_dev_slot& sl = sc->slots[j - 1];
+                            const bool planar = sl.mp < INFINITY &&
+                                                (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_DISK ||
+                                                 sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_RECTANGLE);
+                            if (!planar) { avoid = false; continue; }
+                            anyplanar = true;
+                            const float mm = (sl.mp + sl.mu * S) * 1.001f + pe;
+                            const f3 pos = ld3(sl.pos), a1 = ld3(sl.a1);
+                            const float yA = dot(Ap - pos, a1), yB = dot(Bp - pos, a1);
+                            if (!((yA > mm && yB > mm) || (yA < -mm && yB < -mm))) avoid = false;
+                        }
+                        avoid = avoid && anyspent;
+                        SR_STAT(44, 1);
+                        SR_STAT(47, __popcll(__ballot(trig)));
+                        SR_STAT(48, __popcll(__ballot(avoid)));
+                        SR_STAT(49, __popcll(__ballot(trig && anyplanar)));
+                        SR_STAT(50, __popcll(__ballot(trig && !anyspent && !bhx && T < bs.E[0])));
+                        if (!__ballot(trig && !avoid)) {
+                            SR_STAT(45, 1);
+                            if (iv <= 1) SR_STAT(46, 1);
+                        }
+                        // every triggering lane avoidable or without a spent slot (the ball's margins)
+                        if (!__ballot(trig && !avoid && (anyspent || bhx || !(T < bs.E[0])))) SR_STAT(51, 1);
+                        if (__ballot(avoid)) SR_STAT(52, 1);
+                        if (iv <= 1) SR_STAT(53, 1);
+                    }
+#endif
+#if SR_BALL && !defined(SR_STATS_XCYL) && !defined(SR_STATS_PLANE)  // (SR_STATS_XCYL: counters 44..53 in budget_event instead)
                     if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
                     SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
                     SR_STAT(46, __popcll(__ballot(bhx)));
@@ -2633,7 +2865,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                          fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, r.nv, r.tv,
-                                         cm_iter);
+                                         cm_iter, sjx, e.z, e.w, r.u);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
