@@ -695,8 +695,13 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 // slot's plane the chord's end point lies on (side_slots below); the event
 // happens when a chord's end reaches a slab, a non-side budget runs out, or
 // a lane passes the radius the side tests' margins were sized for.
+// Bit-exact, and events 339.6 k -> 252.8 k per headline frame, but each
+// side stretch replaced about one event (the other slots' budgets end it)
+// and the frame took 3-5 % longer (the side loop's test on 31 % of the
+// wave-steps, the transitions, register pressure; profiles/r04/s21, s22):
+// off.
 #ifndef SR_SIDE
-#define SR_SIDE 1
+#define SR_SIDE 0
 #endif
 #ifndef SR_SIDE_MAX
 #define SR_SIDE_MAX 1  // side slots per wave (1: the kernel's side_j)
