@@ -602,7 +602,7 @@ def main():
 
 
 def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_arg, no_cull, render, first,
-                  restore=(0, 16, 1), frames=20, alone_reps=9, inflight=4):
+                  restore=(0, 16, 1), frames=20, alone_reps=15, inflight=4):
     """Single-frame launches (sr_render_blocks of the whole frame): `alone` =
     one frame at a time, each waited for (median of alone_reps; HIP events on
     the context's stream), `inflight` = `frames` frames in launches of one,
@@ -638,33 +638,42 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
         for _, _, s_k in pool:
             s_k.synchronize()
 
-    def one_alone():
-        rk, tile_k, s_k = pool[0]
-        times = []
-        for j in range(alone_reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            with torch.cuda.stream(s_k):
-                e0.record(s_k)
-                render(rk, (first + j) % n_cam, 1, tile_k, s_k)
-                e1.record(s_k)
-            s_k.synchronize()
-            times.append(e0.elapsed_time(e1))
-        return statistics.median(times)
+    def configure(k, sp, latency):  # context k of the pool: split tiles, latency mode, launch order learned
+        rk, tile_k, s_k = pool[k]
+        rk.set_split(*sp)
+        rk.set_latency_mode(latency)
+        with torch.cuda.stream(s_k):
+            for j in range(2):
+                render(rk, (first + k + j) % n_cam, 1, tile_k, s_k)
+        s_k.synchronize()
 
-    # split tiles (the frame's costliest tiles' rays in sparse waves), then
-    # the default launch, then the latency mode (sr_set_latency_mode: a 2-step
-    # fast loop) without split tiles (with them it measured slower: s8)
-    learn(split)
-    alone = one_alone()
-    learn((0, 16, 1))
-    alone_unsplit = one_alone()
-    for rk, _, _ in pool:
-        rk.set_latency_mode(True)
-    learn((0, 16, 1))
-    alone_latency = one_alone()
+    def time_one(k, j):
+        rk, tile_k, s_k = pool[k]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(s_k):
+            e0.record(s_k)
+            render(rk, (first + j) % n_cam, 1, tile_k, s_k)
+            e1.record(s_k)
+        s_k.synchronize()
+        return e0.elapsed_time(e1)
+
+    # one frame at a time on three contexts of the pool: split tiles (the
+    # frame's costliest tiles' rays in sparse waves), the default launch, and
+    # the latency mode (sr_set_latency_mode: a 2-step fast loop) without split
+    # tiles (with them it measured slower: s8). The three are timed round
+    # robin, so drift in the GPU's state over the measurement (clocks, the
+    # pipeline run before it) reaches all three alike.
+    configure(0, split, False)
+    configure(1, (0, 16, 1), False)
+    configure(2, (0, 16, 1), True)
+    times = [[], [], []]
+    for j in range(alone_reps):
+        for k in range(3):
+            times[k].append(time_one(k, j))
+    alone, alone_unsplit, alone_latency = (statistics.median(t) for t in times)
     for rk, _, _ in pool:
         rk.set_latency_mode(False)
-    learn((0, 16, 1))
+    learn((0, 16, 1))  # the in-flight launches below: default launches on every context
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for j in range(frames):
@@ -681,7 +690,7 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
         rk.close()
     return {
         "alone": {"frames_per_launch": 1, "launches_in_flight": 1, "ms_per_frame": round(alone, 4),
-                  "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events",
+                  "mpix_s": round(W * H / alone / 1e3, 3), "runs": alone_reps, "stat": "median, HIP events, round robin with the two below",
                   "split_tiles": split_arg, "latency_mode": False},
         "alone_default": {"ms_per_frame": round(alone_unsplit, 4), "mpix_s": round(W * H / alone_unsplit / 1e3, 3),
                           "split_tiles": "0", "latency_mode": False},
