@@ -370,7 +370,8 @@ int sr_render_debug(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, 
  * rays finish sooner in sparse waves, at the cost of more waves for those
  * tiles. max_tiles 0 (the default) turns it off. For one
  * headline frame at a time (1920x1080, 2000 steps) sr_set_split(ctx, 32, 16,
- * 1200) measured 1.148 ms against 1.163 ms without (profiles/r04/s16). */
+ * 1200) measured 1.148 ms against 1.163 ms without (profiles/r04/s16), and
+ * 1.067-1.075 ms against 1.106-1.116 ms timed round robin (profiles/r04/s24). */
 int sr_set_split(sr_ctx* ctx, int max_tiles, int lanes_per_wave, int min_steps);
 
 /* Latency mode (not in the reference; the pixels are unchanged): on != 0 runs
