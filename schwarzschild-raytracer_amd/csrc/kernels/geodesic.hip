@@ -605,35 +605,6 @@ __device__ __forceinline__ float plane_window_x(const sr_dev_slot& sl, f3 nv, f3
     return w > 0.0f ? fminf(w, 1000.0f) : 0.0f;  // NaN -> 0
 }
 
-// In-plane distance budget of a planar slot (SR_PLANE2D). Every chord lies in
-// the orbital plane span(nv, tv) (its exact end points within perr of it),
-// where the slot's plane y = (p - pos) . a1 = 0 is the line alpha x + beta y' =
-// g (alpha = nv . a1, beta = tv . a1, g = pos . a1): a point X of the plane at
-// distance R from the ball's centre C has |y(X) - y(C)| <= s R, s = |(alpha,
-// beta)| = the sine of the angle between the two planes. So while |y(C)| - s R
-// exceeds slot_reachable's slab margin m (for chords in that ball: S <= (sqrt 3
-// (|C| + R) + 2 R + 1) 1.001 + perr, perr <= 8e-6 (|C| + R)) plus the rounding
-// of y(C) (a few eps (|C| + |g|)) and of the frame, every chord in the ball
-// misses the slab: R, solved from that linear bound, is the slot's budget. It
-// exceeds the 3-D distance |y| - m by 1 / s: for orbits whose plane lies at a
-// shallow angle to the slot's. 0 when nothing is known (NaN included).
-#ifndef SR_PLANE2D
-#define SR_PLANE2D 1
-#endif
-__device__ __forceinline__ float plane_dist2d(const sr_dev_slot& sl, f3 nv, f3 tv, float cx, float cy) {
-    const f3 a1 = ld3(sl.a1);
-    const float al = dot(nv, a1), be = dot(tv, a1);
-    const float g = dot(ld3(sl.pos), a1);
-    const float y = __builtin_fmaf(al, cx, __builtin_fmaf(be, cy, -g));
-    const float s = __builtin_amdgcn_sqrtf(__builtin_fmaf(al, al, be * be)) * 1.0001f + 1.0e-6f;
-    const float c = fabsf(cx) + fabsf(cy);  // >= |C|
-    const float k0 = (sl.mp + sl.mu * __builtin_fmaf(1.7321f * 1.001f + 8.0e-6f, c, 1.001f)) * 1.001f +
-                     1.0e-5f * (c + fabsf(g)) + 1.0e-4f;
-    const float k1 = sl.mu * (3.7321f * 1.001f + 8.0e-6f) * 1.001f + 1.0e-5f;
-    const float R = (fabsf(y) - k0) * __builtin_amdgcn_rcpf(s + k1) * 0.999f;
-    return R > 0.0f ? R : 0.0f;  // NaN -> 0
-}
-
 // Direction-independent part of a budgeted cylinder's clearance: the distance
 // from A to its height slab (0 <= (p - pos) . axes[1] <= height). cyl_test
 // accepts only a point p = o + lambda d with 0 <= lambda <= len, i.e. on the
@@ -947,8 +918,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 #if SR_BALL
     // the ball's centre: A in the orbital plane (A lies in it: the camera, or a
     // chord end point), within 1e-6 a of A; the budgets give that up
-    const float bcx0 = dot(A, nv), bcy0 = dot(A, tv);
-    bs.setC(bcx0, bcy0);
+    bs.setC(dot(A, nv), dot(A, tv));
     const float m0 = 2.0e-6f * (a + 1.0f);
 #else
     const float m0 = 0.0f;
@@ -988,12 +958,6 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         if (j < nb) nxt = sc->slots[j];
         if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn);
         float e = clearance_obj(sl, A, a) - m0;
-        if (SR_PLANE2D && sl.mp < INFINITY &&
-            (sl.type == SR_OBJECT_RECTANGLE || sl.type == SR_OBJECT_DISK || sl.type == SR_OBJECT_HOLLOW_DISK ||
-             sl.type == SR_OBJECT_PLANE)) {
-            const float w = plane_dist2d(sl, nv, tv, bcx0, bcy0) - m0;
-            e = w > e ? w : e;  // a NaN e stays NaN
-        }
         if (SR_CYL_PLANE && sl.type == SR_OBJECT_CYLINDER && !cyl_par_bit(sc, bs, j)) {
             const float w = plane_window_x(sl, nv, tv, A, SR_MU_QUADRATIC, sl.qk) - m0;
             e = w > e ? w : e;  // a NaN e stays NaN
@@ -1328,14 +1292,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 asm volatile("" : "+v"(ao), "+v"(perr));
                 const float w = plane_window(st, A, B, ao, perr, dphi);
                 v = w > v ? w : v;  // NaN v stays NaN
-            }
-            if (SR_PLANE2D && (TY == SR_OBJECT_RECTANGLE || TY == SR_OBJECT_DISK || TY == SR_OBJECT_HOLLOW_DISK ||
-                               TY == SR_OBJECT_PLANE) && st.mp < INFINITY) {
-                // (the frame recomputed here: held across the slot loop it was spilled)
-                f3 nv_ = nv, tv_ = tv;
-                asm volatile("" : "+v"(nv_.x), "+v"(nv_.y), "+v"(nv_.z), "+v"(tv_.x), "+v"(tv_.y), "+v"(tv_.z));
-                const float w = plane_dist2d(st, nv_, tv_, bs.cx(), bs.cy()) - perr;
-                v = w > v ? w : v;  // a NaN v stays NaN
             }
             if (SR_CYL_PLANE && TY == SR_OBJECT_CYLINDER &&
                 !((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u)) {
