@@ -69,6 +69,12 @@ HEADLINE_PX = 1920 * 1080
 MAX_BATCH = 16  # the bench's cap (the library takes SR_MAX_BATCH = 32)
 
 
+def headline_scale_1gpu(width, height, world):
+    """One GPU and frames of the headline's scale (half to one headline frame
+    of pixels): the shape measured at round 4's kernel (below)."""
+    return world == 1 and HEADLINE_PX // 2 <= width * height <= HEADLINE_PX
+
+
 def frames_per_launch(width, height, world, steps=None):
     """Default frames per launch (sr_render_blocks_batch): a rank's share of B
     frames, B chosen so that one launch carries about eight headline frames'
@@ -79,16 +85,29 @@ def frames_per_launch(width, height, world, steps=None):
     launches in flight overlap each other's ring-wave tails, one cannot
     (profiles/r02/s3_batch_*.jsonl, s12_batch_k20.jsonl: over
     20 frames, 8 / 10 / 10 / 10 frames per launch at N = 1 / 2 / 4 / 8 are
-    within 0.5 % of the best measured)."""
+    within 0.5 % of the best measured). One GPU at the headline's scale: 16
+    frames per launch (two launches in flight, launches_in_flight), and over
+    a short window up to all but four of its frames in the first launch (the
+    second overlaps its tail): at round 4's kernel 16 x 2 renders 1.2 % more
+    frames per second than 8 x 3 over 96 frames and 1.0 % more over the
+    driver's 20 (profiles/r04/s31_shape_96.jsonl, s32_shape_20.jsonl)."""
+    if headline_scale_1gpu(width, height, world):
+        b = MAX_BATCH
+        if steps:
+            b = max(1, min(b, max(-(-steps // 2), steps - 4)))
+        return b
     b = max(1, min(MAX_BATCH, round(8 * HEADLINE_PX * world / (width * height))))
     if steps:
         b = max(1, min(b, -(-steps // 2)))
     return b
 
 
-def launches_in_flight(batch):
+def launches_in_flight(batch, width=0, height=0, world=0):
     """Default launches in flight per GPU (each on its own context and stream):
-    3 for batched launches, 4 for single frames."""
+    3 for batched launches, 4 for single frames; 2 for one
+    GPU's 12 or more headline-scale frames per launch (frames_per_launch)."""
+    if batch >= 12 and headline_scale_1gpu(width, height, world):
+        return 2
     return 3 if batch > 1 else 4
 
 
@@ -179,7 +198,7 @@ def main():
     B = args.batch if args.batch > 0 else frames_per_launch(W, H, world, args.steps)
     if not 1 <= B <= MAX_BATCH:
         raise SystemExit(f"bench: --batch must be 1..{MAX_BATCH}")
-    F = args.inflight if args.inflight > 0 else launches_in_flight(B)
+    F = args.inflight if args.inflight > 0 else launches_in_flight(B, W, H, world)
     split = [int(x) for x in args.split.split(":")] + [16, 1][len(args.split.split(":")) - 1:]
     # every in-flight frame's stream needs a hardware queue of its own (HIP's
     # default is 4 per process); must be set before the HIP runtime starts.

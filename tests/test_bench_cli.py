@@ -58,14 +58,18 @@ def test_frames_per_launch_by_rank_share():
     import bench
 
     # about eight headline frames' worth of a rank's share per launch, 1..16
-    assert [bench.frames_per_launch(1920, 1080, n) for n in (1, 2, 4, 8)] == [8, 16, 16, 16]
+    assert [bench.frames_per_launch(1920, 1080, n) for n in (1, 2, 4, 8)] == [16, 16, 16, 16]
     # at most half of the timed window per launch (two launches overlap their tails)
-    assert [bench.frames_per_launch(1920, 1080, n, 20) for n in (1, 2, 4, 8)] == [8, 10, 10, 10]
+    assert [bench.frames_per_launch(1920, 1080, n, 20) for n in (1, 2, 4, 8)] == [16, 10, 10, 10]
     assert bench.frames_per_launch(1920, 1080, 1, 5) == 3 and bench.frames_per_launch(1920, 1080, 1, 1) == 1
+    assert bench.frames_per_launch(1920, 1080, 1, 8) == 4 and bench.frames_per_launch(1920, 1080, 1, 96) == 16
     assert bench.frames_per_launch(640, 360, 1) == 16  # config 2
     assert bench.frames_per_launch(3840, 2160, 1) == 2 and bench.frames_per_launch(3840, 2160, 8) == 16
     assert bench.frames_per_launch(7680, 4320, 1) == 1 and bench.frames_per_launch(7680, 4320, 8) == 4
     assert bench.launches_in_flight(4) == 3 and bench.launches_in_flight(1) == 4
+    # one GPU at the headline's scale: 16 frames per launch, two in flight
+    assert bench.launches_in_flight(16, 1920, 1080, 1) == 2 and bench.launches_in_flight(16, 1920, 1080, 2) == 3
+    assert bench.launches_in_flight(16, 640, 360, 1) == 3 and bench.launches_in_flight(4, 1920, 1080, 1) == 3
     a = _parse(["--batch", "2", "--split", "32:4:1000"])
     assert a.batch == 2 and a.split == "32:4:1000"
 
