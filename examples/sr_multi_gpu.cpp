@@ -74,7 +74,7 @@ namespace {
 constexpr int kBlockRows = 8;  // one 8x8 wave tile tall
 
 struct Args {
-    int gpus = 1, width = 1920, height = 1080, max_steps = 2000, frames = 20, batch = 8, warmup = 24, inflight = 3;
+    int gpus = 1, width = 1920, height = 1080, max_steps = 2000, frames = 20, batch = 16, warmup = 32, inflight = 2;
     bool flyby = false;
     bool force_gather = false;  // N = 1 too: price, gather (one rank) and reassemble (tests that path)
     std::string skybox, array, out_raw, id_file;

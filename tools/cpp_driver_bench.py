@@ -6,7 +6,7 @@ frames per launch, F launches in flight, K timed frames). Prints one JSON
 line per run and a summary line; the driver's last frame is checked against
 the oracle's row hashes (tests/golden/frame_hashes.npz c3).
 
-  python tools/cpp_driver_bench.py [--rounds 3] [--frames 20] [--batch 8] [--inflight 3]
+  python tools/cpp_driver_bench.py [--rounds 3] [--frames 20] [--batch 16] [--inflight 2]
 """
 import argparse
 import hashlib
@@ -27,9 +27,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--frames", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=8)
-    ap.add_argument("--inflight", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=24)
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--inflight", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=32)
     args = ap.parse_args()
     import srpkg
 
