@@ -1,5 +1,6 @@
 #!/bin/bash
-# r4 s42: stream priorities of the two launch slots (SR_BENCH_STREAM_PRIO),
+# r4 s42: stream priorities of the two launch slots (SR_BENCH_STREAM_PRIO: a
+# timing-only bench.py option of that session, removed after it),
 # 96 and 20 frames, interleaved with the default
 cd "${GRAFT_REPO_ROOT}" || exit 1
 export TMPDIR=/tmp
