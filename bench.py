@@ -22,7 +22,7 @@ kernel source and config) over the same timed run's frame time - and the
 reference's CPU press-R geodesic loop swept over a sample of the frame's
 pixels on this host (cpu_baseline; oracle restatement, "port").
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W]   (N > 1: spawns N ranks, launch_contract)
   torchrun --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -187,8 +187,87 @@ def parse():
     return ap.parse_args()
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str], grace_s: float = 30.0) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run N rank
+    processes of this script, one per GPU, with the env:// rendezvous
+    torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT). This parent
+    imports neither torch nor HIP. The ranks share its stdout, so rank 0's JSON
+    line is the run's line. Returns the first non-zero exit status (in the
+    order the ranks failed), else 0; once a rank has failed the others get
+    `grace_s` to finish before they are terminated (they would otherwise wait
+    in a collective for the dead rank)."""
+    import signal
+
+    port = free_port()
+    script = str(Path(__file__).resolve())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
+
+    def stop(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+    old = signal.signal(signal.SIGTERM, lambda *a: (stop(), sys.exit(143)))
+    first_bad, failed_at = 0, None
+    try:
+        while any(p.poll() is None for p in procs):
+            for p in procs:
+                rc = p.poll()
+                if rc not in (None, 0) and first_bad == 0:
+                    first_bad, failed_at = rc, time.monotonic()
+                    print(f"bench: rank {procs.index(p)} exited with status {rc}", file=sys.stderr)
+            if failed_at is not None and time.monotonic() - failed_at > grace_s:
+                stop()
+                break
+            time.sleep(0.05)
+        for p in procs:
+            rc = p.wait()
+            if rc != 0 and first_bad == 0:
+                first_bad = rc
+    finally:
+        stop()
+        signal.signal(signal.SIGTERM, old)
+    return 1 if first_bad < 0 else first_bad  # a signal-killed rank (negative rc) is a failure too
+
+
+def launch_contract(args) -> None:
+    """The driver's launch shapes: `bench.py --gpus N` under
+    torch.distributed.run (WORLD_SIZE set by the launcher: it must equal N),
+    or alone (N > 1: spawn_ranks; N = 1: this process renders)."""
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != args.gpus:
+            raise SystemExit(f"bench: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}: "
+                             "run one rank per GPU (--nproc-per-node equal to --gpus)")
+        return
+    if args.gpus > 1:
+        sys.stdout.flush()
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+
+
 def main():
     args = parse()
+    launch_contract(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -220,7 +299,14 @@ def main():
 
     pkg = srpkg.load_package()
     abi, sc = pkg.abi, pkg.scenes
-    ndev = max(1, torch.cuda.device_count())
+    ndev_seen = torch.cuda.device_count()  # counts devices without initialising HIP
+    if distributed and args.dist_backend == "nccl":
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        if ndev_seen < local_world:
+            # RCCL needs a GPU per rank: two ranks on one device hang or fail in init
+            raise SystemExit(f"bench: --dist-backend nccl needs one GPU per rank: {local_world} local ranks but "
+                             f"{ndev_seen} visible device(s) (use --dist-backend gloo to rehearse on fewer GPUs)")
+    ndev = max(1, ndev_seen)
     dev = torch.device("cuda", local % ndev)
     if distributed:
         if args.dist_backend == "nccl":

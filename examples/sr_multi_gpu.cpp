@@ -22,7 +22,7 @@
 //
 // Two ways to run it:
 //   one process, N GPUs     ./sr_multi_gpu --gpus N ...        (ncclCommInitAll)
-//   one process per GPU     RANK=r WORLD_SIZE=N LOCAL_RANK=r ./sr_multi_gpu --id-file F ...
+//   one process per GPU     RANK=r WORLD_SIZE=N LOCAL_RANK=r ./sr_multi_gpu [--id-file F] ...
 //                           (ncclCommInitRank; rank 0 writes the unique id to F,
 //                           prices the blocks and ncclBroadcasts the lists)
 // Textures: raw files (--skybox PATH:W:H with RGB8 rows bottom-up, --array
@@ -32,12 +32,15 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <fstream>
+#include <sys/stat.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -214,8 +217,27 @@ void setup_slot(Slot& s, int dev, const Args& a, const sr_scene& scene, size_t t
 
 }  // namespace
 
+// One process per GPU: the file through which rank 0 hands the RCCL unique id
+// to the other ranks. --id-file, else a name unique to the launch: the
+// launcher's run id (TORCHELASTIC_RUN_ID) and rendezvous port (MASTER_PORT),
+// so concurrent or earlier runs with other ports never share a file. Ranks > 0
+// also reject a file older than themselves (main's stat check), and rank 0
+// removes it once every rank has joined.
+constexpr time_t kIdSkewS = 30;  // launcher start-up skew allowed between ranks
+
+static std::string id_file_path(const std::string& given) {
+    if (!given.empty()) return given;
+    const char* run = std::getenv("TORCHELASTIC_RUN_ID");
+    const char* port = std::getenv("MASTER_PORT");
+    std::string p = "/tmp/sr_multi_gpu";
+    if (run && *run && std::strcmp(run, "none") != 0) p += std::string(".") + run;
+    if (port && *port) p += std::string(".") + port;
+    return p + ".ncclid";
+}
+
 int main(int argc, char** argv) {
-    const Args a = parse(argc, argv);
+    const time_t t_start = std::time(nullptr);
+    Args a = parse(argc, argv);
     const char* ws = std::getenv("WORLD_SIZE");
     const bool per_process = ws && std::atoi(ws) > 1;
     const int world = per_process ? std::atoi(ws) : a.gpus;
@@ -232,6 +254,10 @@ int main(int argc, char** argv) {
         return 1;
     }
     const int W = a.width, H = a.height, B = a.batch, F = a.inflight;
+    // warmup of at least one launch per slot: a slot's context learns its launch
+    // order from its own first launch, so an unwarmed slot's first timed launch
+    // would run in the default order
+    a.warmup = std::max(a.warmup, B * F);
     const bool gather = world > 1 || a.force_gather;  // N = 1: the tile is the frame
     const int nb = (H + kBlockRows - 1) / kBlockRows, nc = (W + 7) / 8;
     const int per = (nb + world - 1) / world;
@@ -256,18 +282,23 @@ int main(int argc, char** argv) {
     if (per_process) {
         devs[0].dev = local % ndev;
         ncclUniqueId id;
-        const std::string path = a.id_file.empty() ? std::string("/tmp/sr_multi_gpu.ncclid") : a.id_file;
+        const std::string path = id_file_path(a.id_file);
         if (rank == 0) {
             CHECK_NCCL(ncclGetUniqueId(&id));
             const std::string tmp = path + ".tmp";
             std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(&id), sizeof id);
             std::rename(tmp.c_str(), path.c_str());
         } else {
+            // a file older than this process (minus the launcher's start-up
+            // skew) is a previous run's: never hand its id to ncclCommInitRank
             for (int t = 0;; t++) {
-                std::ifstream f(path, std::ios::binary);
-                if (f.read(reinterpret_cast<char*>(&id), sizeof id)) break;
+                struct stat st;
+                if (::stat(path.c_str(), &st) == 0 && st.st_mtime + kIdSkewS >= t_start) {
+                    std::ifstream f(path, std::ios::binary);
+                    if (f.read(reinterpret_cast<char*>(&id), sizeof id)) break;
+                }
                 if (t > 6000) {
-                    std::fprintf(stderr, "rank %d: no NCCL id in %s\n", rank, path.c_str());
+                    std::fprintf(stderr, "rank %d: no NCCL id of this run in %s\n", rank, path.c_str());
                     return 1;
                 }
                 std::this_thread::sleep_for(std::chrono::milliseconds(10));
@@ -275,6 +306,8 @@ int main(int argc, char** argv) {
         }
         CHECK_HIP(hipSetDevice(devs[0].dev));
         CHECK_NCCL(ncclCommInitRank(&devs[0].comm, world, id, rank));
+        // every rank has joined once rank 0's init returns: no later run can read this id
+        if (rank == 0) std::remove(path.c_str());
     } else {
         std::vector<ncclComm_t> comms(world);
         std::vector<int> ids(world);

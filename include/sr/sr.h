@@ -273,7 +273,12 @@ int sr_set_test_ray(sr_ctx* ctx, const sr_test_ray* test_ray);
  * dev_rgba8 + (r - row_begin) * pitch_bytes). Asynchronous on `stream`.
  * A context reuses its per-frame scratch (pixel state, launch order), so its
  * renders are ordered: a launch on another stream than the context's last
- * one first waits (hipStreamWaitEvent) for the work of that stream. */
+ * one first waits (hipStreamWaitEvent on an event recorded at the end of that
+ * launch) for the work of that stream. Between launches the context frees
+ * replaced buffers in stream order on its last launch's stream, and the calls
+ * that wait for the context's frames (sr_set_*, sr_wave_costs, sr_destroy)
+ * synchronise it: keep that stream alive until the context's next launch (on
+ * any stream) or sr_destroy. */
 int sr_render(sr_ctx* ctx, const sr_camera* cam, const sr_params* params, int width,
               int height, int row_begin, int row_end, uint8_t* dev_rgba8,
               size_t pitch_bytes, sr_stream stream);

@@ -697,10 +697,14 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.wave_cost = d_wave_cost;
     if (!hip_ok(hipSetDevice(ctx->device))) return SR_E_HIP;
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (ctx->launched && s != ctx->last_stream) {  // ordered after the launches on the previous stream
-        if (!hip_ok(hipEventRecord(ctx->order_ev, ctx->last_stream)) || !hip_ok(hipStreamWaitEvent(s, ctx->order_ev, 0)))
-            return SR_E_HIP;
+    if (ctx->launched && s != ctx->last_stream) {
+        // ordered after the launches on the previous stream: order_ev was
+        // recorded at the end of the last launch, so the old stream's handle
+        // is not touched here (the caller may have destroyed it since)
+        if (!hip_ok(hipStreamWaitEvent(s, ctx->order_ev, 0))) return SR_E_HIP;
     }
+    // every stream-ordered free from here on (ensure_*'s evictions) goes to s
+    ctx->last_stream = s;
     const float4* tbl = nullptr;
     rc = ensure_table(ctx, params->max_steps, params->max_revolutions, s, &tbl);
     if (rc != SR_OK) return rc;
@@ -720,7 +724,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
                                       ctx->d_diag,
                                       ctx->timing_n < ctx->timing_cap ? &ctx->tev[4 * (size_t)ctx->timing_n++] : nullptr,
                                       s);
-    ctx->last_stream = s;
+    if (hip_ok(e)) e = hipEventRecord(ctx->order_ev, s);
     ctx->launched = true;
     return hip_ok(e) ? SR_OK : SR_E_HIP;
 }

@@ -88,3 +88,60 @@ def test_cpu_baseline_sweeps_the_full_frame():
     assert out["like_for_like"]["value"] == 0.00225
     part = bench.cpu_baseline(cam, 48, 27, 60, 9, sweeps=(), rays=())
     assert part["sample"].startswith("sample: ") and "rows [9,18)" in part["sample"]
+
+
+def _bench(args, env_extra=None, timeout=120):
+    import os
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=ROOT)
+
+
+def test_world_size_must_equal_gpus():
+    """A launcher's WORLD_SIZE that differs from --gpus is an error (before
+    any torch or HIP import), not a mislabelled line."""
+    r = _bench(["--gpus", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"}, timeout=30)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr and "--gpus 1" in r.stderr
+    r = _bench(["--gpus", "4"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"}, timeout=30)
+    assert r.returncode != 0 and "--gpus 4" in r.stderr
+    r = _bench(["--gpus", "0"], timeout=30)
+    assert r.returncode != 0
+
+
+def test_spawned_ranks_need_a_gpu_each_for_nccl():
+    """--gpus 2 without a launcher spawns two ranks (launch_contract); with
+    the nccl backend and fewer visible GPUs than local ranks (none here) every
+    rank exits non-zero at once with the reason, and so does the parent."""
+    import time
+
+    t = time.monotonic()
+    r = _bench(["--gpus", "2", "--dist-backend", "nccl", "--steps", "2"], {"HIP_VISIBLE_DEVICES": ""}, timeout=120)
+    assert r.returncode != 0
+    assert r.stderr.count("needs one GPU per rank: 2 local ranks") == 2, r.stderr[-2000:]
+    assert time.monotonic() - t < 60
+
+
+def test_spawn_ranks_env_and_status(tmp_path):
+    """spawn_ranks gives each rank the env:// rendezvous of
+    torch.distributed.run and returns the first failure's status."""
+    import bench
+
+    probe = tmp_path / "probe.py"
+    probe.write_text("import json, os, sys\n"
+                     "keys = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT')\n"
+                     f"open(r'{tmp_path}/rank' + os.environ['RANK'], 'w').write(json.dumps({{k: os.environ[k] for k in keys}}))\n"
+                     "sys.exit(int(sys.argv[1]) if os.environ['RANK'] == sys.argv[2] else 0)\n")
+    old = bench.__file__
+    try:
+        bench.__file__ = str(probe)
+        assert bench.spawn_ranks(3, ["0", "-1"]) == 0
+        envs = [json.loads((tmp_path / f"rank{r}").read_text()) for r in range(3)]
+        assert [e["RANK"] for e in envs] == ["0", "1", "2"] and [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2"]
+        assert all(e["WORLD_SIZE"] == "3" and e["LOCAL_WORLD_SIZE"] == "3" and e["MASTER_ADDR"] == "127.0.0.1"
+                   for e in envs)
+        assert len({e["MASTER_PORT"] for e in envs}) == 1
+        assert bench.spawn_ranks(2, ["7", "1"], grace_s=5) == 7
+    finally:
+        bench.__file__ = old

@@ -76,3 +76,39 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
         assert np.array_equal(fa, fb), a.name
         distinct.add(fa.tobytes())
     assert len(distinct) == 12  # the flyby moves the camera every frame
+
+
+def test_bench_gpus_2_without_a_launcher(tmp_path):
+    """The driver's BENCH command shape with N = 2 and no torchrun: bench.py
+    spawns its two ranks itself (launch_contract; gloo here, both on the one
+    GPU), labels the line with them, and its last timed headline frame matches
+    the oracle's frame hashes."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--steps", "4",
+                        "--warmup", "2", "--cpu-baseline", "off", "--critical-path", "off", "--reference-loop", "off"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]  # rank 0's line only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size"] == 2
+    assert [x["rank"] for x in d["config"]["ranks"]] == [0, 1]
+    assert d["parity"]["frame_sha_match"] is True, d["parity"]
+
+
+def test_bench_nccl_refuses_two_ranks_on_one_gpu():
+    """--gpus 2 with RCCL on a one-GPU box: a clear, quick failure instead of
+    two RCCL ranks on one device."""
+    import time
+
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except ImportError:
+        pytest.skip("torch missing")
+    if n >= 2:
+        pytest.skip("more than one GPU visible")
+    t = time.monotonic()
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "nccl", "--steps", "2"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "needs one GPU per rank" in r.stderr, r.stderr[-2000:]
+    assert time.monotonic() - t < 60
