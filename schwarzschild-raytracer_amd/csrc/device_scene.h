@@ -205,6 +205,10 @@ typedef struct {
     // latency mode (sr_set_latency_mode: one frame alone ~5 % sooner, frames
     // in flight ~0.5 % slower)
     int32_t fast_unroll;
+    // S_max = (sqrt 3 + 3) R + 1 (x 1.001, rounded up) for R = 1 / u_f: bounds
+    // |o|_1 + len + 1 of every chord from inside the u_f sphere to within 2 R
+    // (geodesic.hip budget_frame's orbital-plane exclusion); +inf when u_f <= 0
+    float xplane_s;
 } sr_dev_frame;
 
 #endif

@@ -23,11 +23,6 @@ __device__ __forceinline__ float4 ldc(const sr_cfloat4* p) {
     const sr_v4f v = *p;
     return make_float4(v.x, v.y, v.z, v.w);
 }
-// the compact step table (SR_CTABLE): 5 floats per step, dword aligned
-typedef float sr_v8f_a4 __attribute__((ext_vector_type(8), aligned(4)));
-typedef float sr_v16f_a4 __attribute__((ext_vector_type(16), aligned(4)));
-typedef const __attribute__((address_space(4))) sr_v8f_a4 sr_cf8a;
-typedef const __attribute__((address_space(4))) sr_v16f_a4 sr_cf16a;
 
 #include "../device_scene.h"
 
@@ -373,17 +368,12 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 // a window of path W holds for chords within a ball of radius W, except the
 // chord length (up to 2 W) and the directional plane window (a path bound,
 // converted in plane_window).
-#ifndef SR_BALL
-#define SR_BALL 1
-#endif
 #ifndef SR_NEAR
 #define SR_NEAR 1.0f
 #endif
 #ifndef SR_XPLANE  // orbital-plane exclusion of bounded slots (budget_frame)
 #define SR_XPLANE 1
 #endif
-// |o|_1 + len + 1 of a chord whose ends lie within r = 110: sqrt(3) 110 + 220 + 1 <= 412
-#define SR_XPLANE_S 420.0f
 // The margin factor of a slot's distance tests: a planar primitive's
 // per-chord factor (SR_MU_PLANAR: it accepts a chord point within a few eps
 // S of its plane and bounds), the quadratic one for spheres and cylinders
@@ -433,7 +423,7 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
             // origins stay within sqrt(3) W of A, chords within W long
             const float W = fminf(c, SR_BUDGET_TMAX);
             // (chords of a ball of radius W are up to 2 W long: SR_BALL)
-            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + ((SR_BALL ? 4.0f : 3.0f) * W + 1.0f);
+            float Sb = (fabsf(A.x) + fabsf(A.y) + fabsf(A.z)) + sl.pl1 + (4.0f * W + 1.0f);
             float qm = (Sb * Sb) * sl.qk;
             c = fminf(c - qm, SR_BUDGET_TMAX);
         }
@@ -504,16 +494,11 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     if (!(R > 0.0f)) return 0.0f;
     const float b = c + th0;
     const float L = (__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, 2.0f * kap * R)) - b) * (a2 * (1.0f / 6.06f));
-#if SR_BALL
     const float ch = 1.5f * a * dphi;  // the next chord
     const float Lc = fminf(L, fminf(__builtin_fmaf(0.5f, a, -ch), (1.5f - th0) * (a2 * (1.0f / 6.06f)) - ch));
     const float th1 = __builtin_fmaf(kap, Lc, th0);
     const float f = 1.0f - (th1 * th1 + th1 * th0 + th0 * th0) * (1.0f / 6.0f);
     return (Lc > 0.0f && f > 0.0f) ? Lc * f * 0.998f : 0.0f;
-#else
-    (void)dphi;
-    return fminf(L, 0.5f * a) * 0.998f;
-#endif
 }
 // slot j >= 1 for an outward lane at distance a (cyl_par: bs.cm's bit for a budgeted cylinder)
 __device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par, float a, float dip) {
@@ -553,56 +538,6 @@ __device__ __forceinline__ sr_dev_slot pin_slot(const sr_dev_slot& g) {
     SR_PIN(sl.a2[1]);
     SR_PIN(sl.a2[2]);
     return sl;
-}
-
-// Plane window of a budgeted cylinder (SR_CYL_PLANE, round 4): a budget
-// from the orbital plane instead of the distance to the cylinder. Every chord
-// of the orbit lies within 1e-6 r + 1e-4 of the plane span(nv, tv) through the
-// origin (its binary32 end points, as budget_frame's exclusion), so it passes
-// at least hx - that from the bounding centre bc, hx = |bc . n| / |n|. When no
-// chord of the orbit can be nearly parallel to the axis (bs.cm's bit clear:
-// |d_perp|^2 >= 2 SR_BUDGET_DPMIN), may_hit lets a chord reach the cylinder
-// only within br + mu S + qk (S + |pos|_1)^2 of bc (qk = SR_CYL_QMARGIN /
-// (r SR_BUDGET_DPMIN) covers the quadratic's root error with a factor 2 to
-// spare; mu the quadratic factor, above the planar one may_hit uses), S = |o|_1
-// + len + 1. So chords with S <= S_max, the largest S at which that reach is
-// below hx less the rounding, cannot be hit; the chords in a ball of radius W
-// around the anchor C have S <= |C|_1 + (2 + sqrt 3) W + 1 (origins within W
-// of C, lengths within 2 W): the budget is the W for S_max. It replaces the
-// distance budget when larger (lanes passing the cylinder off its plane:
-// 90 % of the cylinder's re-anchors, profiles/r04/s11_stats_xcyl.json).
-// Returns 0 when the plane is too near (or the frame NaN). Measured
-// (profiles/r04/s12_*, frames bit-identical): the cylinder's re-anchors 124.5 k
-// -> 49.6 k per headline frame, but events 339.6 k -> 345.3 k (the events the
-// cylinder no longer triggers re-anchored other slots ahead of their own
-// expiry) and the frame time unchanged (0.848 vs 0.849 ms); off.
-#ifndef SR_CYL_PLANE
-#define SR_CYL_PLANE 0
-#endif
-// SR_QPLANE: the same window for spheres and boxes (no quadratic term: their
-// reach is br + mu S in every direction, mu their own factor); planes far
-// enough from them are excluded outright (budget_frame). Measured with the
-// cylinder's (s12): sphere re-anchors 21.8 k -> 16.5 k, events 345.3 k ->
-// 341.7 k, frame time +0.7 %; off.
-#ifndef SR_QPLANE
-#define SR_QPLANE 0
-#endif
-__device__ __forceinline__ float plane_window_x(const sr_dev_slot& sl, f3 nv, f3 tv, f3 C, float mu, float q) {
-    const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
-    const float hx = fabsf(dot(ld3(sl.bc), n)) * __builtin_amdgcn_rsqf(dot(n, n)) * (1.0f - 1.0e-5f);
-    // room for the reach: hx less the chords' distance from the plane (end
-    // points within 1e-6 r + 1e-4 of it, r <= |C| + 3 W <= 3100 for W <= 1000)
-    // and the rounding of hx, then the bounding radius
-    const float room = (hx - (3.2e-3f + 1.0e-5f * sl.cn)) * (1.0f / 1.001f) - sl.br;
-    if (!(room > 0.0f)) return 0.0f;
-    // largest x = S + |pos|_1 with qk x^2 + mu x <= room + mu |pos|_1 (the
-    // positive root in its cancellation-free form)
-    const float c = room + mu * sl.pl1;
-    const float x = 2.0f * c / (mu + __builtin_amdgcn_sqrtf(__builtin_fmaf(4.0f * q, c, mu * mu)));
-    const float smax = (x - sl.pl1) * 0.999f;
-    const float c1 = fabsf(C.x) + fabsf(C.y) + fabsf(C.z);
-    const float w = (smax * (1.0f / 1.001f) - c1 - 1.0f) * (1.0f / 3.7321f) * 0.999f;
-    return w > 0.0f ? fminf(w, 1000.0f) : 0.0f;  // NaN -> 0
 }
 
 // Direction-independent part of a budgeted cylinder's clearance: the distance
@@ -649,22 +584,6 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
-// The fast loop's compact step table (SR_CTABLE = 1): 5 floats per step
-// {step_size, step_size / 6, cos phi, sin phi, 0.5 step_size}, after the main
-// table's 2 (max_steps + 4) float4 (sr_api.cpp ensure_table), so that one
-// iteration's three entries are a single 16-dword scalar load (15 used)
-// instead of six float4 (24 SGPRs). 8 fewer SGPRs live through the fast loop
-// and no VGPR spills in the hot instantiation, but the compiler then rotates
-// u, u' and the previous u through extra moves (44 VALU per step instead of
-// 42.3) and the pipeline renders 7.4 % fewer frames per second (0.972 vs
-// 0.903 ms per frame, interleaved, profiles/r04/s4_ab_tp.log and
-// s5_ab_tp.log; one frame alone 1.4 % sooner). Off: the headline is throughput.
-#ifndef SR_CTABLE
-#define SR_CTABLE 0
-#endif
-#if SR_CTABLE && !SR_BALL
-#error "SR_CTABLE drops the entries (g, K) only the SR_BALL = 0 step bound reads"
-#endif
 #ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries);
                         // the latency mode's instantiation runs 2 (sr_set_latency_mode)
 #define SR_FAST_UNROLL 3
@@ -686,38 +605,13 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 // registers (held in VGPRs across it they were spilled to scratch and
 // reloaded at every event). The default scene's kernel (6 slots, 1 cylinder)
 // takes 17 rows, 4.25 KiB per 64-lane wave.
-// Side slots (SR_SIDE). A planar slot's distance budget runs out long before
-// most lanes' chords come near the primitive's plane: half of the headline's
-// budget events (168 k of 340 k per frame, profiles/r04/s20) had only planar
-// slots spent, by lanes whose chord stayed off those slots' acceptance slabs
-// (slot_reachable). At such an event the wave instead takes those slots (at
-// most SIDE of them) out of its ball and tests, per step, the side of each
-// slot's plane the chord's end point lies on (side_slots below); the event
-// happens when a chord's end reaches a slab, a non-side budget runs out, or
-// a lane passes the radius the side tests' margins were sized for.
-// Bit-exact, and events 339.6 k -> 252.8 k per headline frame, but each
-// side stretch replaced about one event (the other slots' budgets end it)
-// and the frame took 3-5 % longer (the side loop's test on 31 % of the
-// wave-steps, the transitions, register pressure; profiles/r04/s21, s22):
-// off.
-#ifndef SR_SIDE
-#define SR_SIDE 0
-#endif
-#ifndef SR_SIDE_MAX
-#define SR_SIDE_MAX 1  // side slots per wave (1: the kernel's side_j)
-#endif
 template <int NB, int NC>
 struct BudgetLayout {
     static constexpr int PA0 = NB + 1;
     static constexpr int SLAB0 = PA0 + 2 * NC;
     static constexpr int BT = SLAB0 + NC;
     static constexpr int BM = BT + 1, BCX = BT + 2, BCY = BT + 3, BMH = BT + 4, BCM = BT + 5, BUHI = BT + 6;
-    // side slots (SR_SIDE; the small layout only): the ball without them
-    // (QS), the u bound of the side tests' radius (US), and per side slot s
-    // the test's coefficients in rows SP0 + 3 s .. SP0 + 3 s + 2
-    static constexpr int SIDE = (SR_SIDE && NB <= 6 && NC <= 1) ? SR_SIDE_MAX : 0;
-    static constexpr int QS = BT + 7, US = BT + 8, SP0 = BT + 9;
-    static constexpr int ROWS = BT + 7 + (SIDE ? 2 + 3 * SIDE : 0);
+    static constexpr int ROWS = BT + 7;
 };
 // The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
@@ -826,9 +720,6 @@ struct Budget {
         st(L::BCM, __uint_as_float(cm | (excl << 8)));
     }
     __device__ __forceinline__ float uhi() const { return ld(L::BUHI); }
-    __device__ __forceinline__ float qs() const { return ld(L::QS); }
-    __device__ __forceinline__ float us() const { return ld(L::US); }
-    __device__ __forceinline__ float sp(int s, int k) const { return ld(L::SP0 + 3 * s + k); }
     __device__ __forceinline__ void setUhi(float v) const { st(L::BUHI, v); }
     static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
@@ -847,10 +738,13 @@ struct Budget {
 // this orbit can be near-parallel to the axis and bit k of bs.cm stays clear:
 // chord_parallel skips the cylinder for this lane.
 // slot j's orbital-plane exclusion bit (below), n = nv x tv, nn = |n|^2
-__device__ __forceinline__ uint32_t xplane_bit(const sr_dev_slot& sl, int j, f3 n, float nn) {
+// (xs = sr_dev_frame.xplane_s: S_max of the orbit's chords, +inf: no
+// exclusion; it carries 0.5 % on top, which covers the end points' 4e-7 r
+// off the plane as mu >= SR_MU_PLANAR)
+__device__ __forceinline__ uint32_t xplane_bit(const sr_dev_slot& sl, int j, f3 n, float nn, float xs) {
     if (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_CYLINDER) return 0u;
     const float h = dot(ld3(sl.bc), n);  // |h| / |n|: bc's distance from the plane
-    const float need = (sl.br + sl.mu * SR_XPLANE_S) * 1.001f + 1.0e-4f + 1.0e-5f * sl.cn;
+    const float need = (sl.br + sl.mu * xs) * 1.001f + 1.0e-4f + 1.0e-5f * sl.cn;
     // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
     return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
 }
@@ -874,7 +768,7 @@ __device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restr
     return cm;
 }
 template <class BS>
-__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
+__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv, float xs) {
     const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
     uint32_t x = 0;
 #if SR_XPLANE
@@ -882,20 +776,24 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
     // end points (nv cos phi + tv sin phi) / u computed in binary32, within
     // 4e-7 r of the plane span(nv, tv) through the origin, and an object's
     // exact test accepts only points within br + mu S of its bounding
-    // sphere's centre bc (may_hit). So when bc lies farther from that plane
-    // than br + mu S_max (S_max = SR_XPLANE_S bounds |o|_1 + len + 1 for chords
-    // whose ends lie within r = 110, the u_f sphere's exit chords included,
-    // as outward_clear assumes) plus the rounding, no chord of the orbit can
-    // reach the object: its budget is +inf until the next reseed (a new
-    // plane). Planes (unbounded) and cylinders (their quadratic margin grows
-    // near the axis direction) are never excluded. Of the default scene the
-    // sphere and the box lie off most rays' planes (the pencil of planes
+    // sphere's centre bc (may_hit). Every applied step of an orbit but its
+    // last has u >= u_f, so a chord starts within R = 1 / u_f, and it ends
+    // within 2 R unless it is that last one (the step to u < u_f: a reseed or
+    // the ray's end follows) with u < u_f / 2. So S = |o|_1 + len + 1 <=
+    // (sqrt 3 + 3) R + 1 = S_max (sr_dev_frame.xplane_s, the host's bound,
+    // +inf when u_f <= 0), and when bc lies farther from that plane than br +
+    // mu S_max plus the rounding, no such chord can reach the object: its
+    // budget is +inf until the next reseed (a new plane). A chord ending
+    // beyond 2 R is an event with the excluded slots forced (integrate,
+    // budget_event: rare, a near-radial escape). Planes (unbounded) and cylinders (their quadratic margin
+    // grows near the axis direction) are never excluded. Of the default scene
+    // the sphere and the box lie off most rays' planes (the pencil of planes
     // through the camera and the hole).
     {
         const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
         const float nn = dot(n, n);
         const int nb = sc->num_budget;
-        for (int j = 1; j <= nb; j++) x |= xplane_bit(sc->slots[j - 1], j, n, nn);
+        for (int j = 1; j <= nb; j++) x |= xplane_bit(sc->slots[j - 1], j, n, nn, xs);
     }
 #endif
     bs.setCm(cm, x);
@@ -911,18 +809,14 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 
 template <class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
-                                            bool outward, float dip, bool bh_ok, bool falling) {
+                                            bool outward, float dip, bool bh_ok, bool falling, float xs) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.setT(0.0f);
-#if SR_BALL
     // the ball's centre: A in the orbital plane (A lies in it: the camera, or a
     // chord end point), within 1e-6 a of A; the budgets give that up
     bs.setC(dot(A, nv), dot(A, tv));
     const float m0 = 2.0e-6f * (a + 1.0f);
-#else
-    const float m0 = 0.0f;
-#endif
     float m = INFINITY;
     // the cm bits first (outward_slot); the exclusion bits in the slot loop
     const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
@@ -956,16 +850,8 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     for (int j = 1; j <= nb; j++) {
         const sr_dev_slot sl = pin_slot(nxt);
         if (j < nb) nxt = sc->slots[j];
-        if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn);
+        if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn, xs);
         float e = clearance_obj(sl, A, a) - m0;
-        if (SR_CYL_PLANE && sl.type == SR_OBJECT_CYLINDER && !cyl_par_bit(sc, bs, j)) {
-            const float w = plane_window_x(sl, nv, tv, A, SR_MU_QUADRATIC, sl.qk) - m0;
-            e = w > e ? w : e;  // a NaN e stays NaN
-        }
-        if (SR_QPLANE && (sl.type == SR_OBJECT_SPHERE || sl.type == SR_OBJECT_BOX)) {
-            const float w = plane_window_x(sl, nv, tv, A, sl.mu, 0.0f) - m0;
-            e = w > e ? w : e;
-        }
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
         bs.E[j * SR_E_STRIDE] = e;
@@ -1125,8 +1011,7 @@ template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
-                                                 bool falling, f3 nv, f3 tv, bool par_recompute,
-                                                 int sj, float sc_, float ss_, float su_) {
+                                                 bool falling, bool par_recompute, float u_f) {
     constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
@@ -1166,16 +1051,8 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         par &= bs.cm();
     }
     // this lane's slots whose E does not cover the chord (bit 0: the chord
-    // left the black hole's u window, bhx; side slots: their side test)
+    // left the black hole's u window, bhx)
     uint32_t forced = (uint32_t)bhx;
-    if (BS::L::SIDE > 0 && sj > 0) {
-        // the side slot (side_slots), forced where its side test failed at
-        // this chord's end (cos, sin, u) = (sc_, ss_, su_) or the lane passed
-        // the radius bound (recomputed here: carried from the step loop's
-        // exit, the mask was spilled)
-        const float w = __builtin_fmaf(bs.sp(0, 0), sc_, __builtin_fmaf(bs.sp(0, 1), ss_, -bs.sp(0, 2) * su_));
-        forced |= (uint32_t)(!(w > 0.0f) || su_ < bs.us()) << sj;
-    }
     {
         uint32_t c = cyl;
 #pragma unroll
@@ -1188,6 +1065,10 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         }
     }
     if (reanchor_cyl) forced |= (2u << nb) - 1u;  // a new orbital frame: outward budgets start over
+    // the orbital-plane exclusions hold for chords ending within 2 / u_f
+    // (budget_frame): beyond (|B| >= 2 / u_f (1 - 1e-5) > 1.9 / u_f for a
+    // chord to u < u_f / 2, integrate's event) this lane's excluded slots are forced
+    if (SR_XPLANE && dot(B, B) * (u_f * u_f) > 3.61f) forced |= bs.excl();
     uint32_t spent = 0;  // wave-uniform: slots some lane has spent or is about to
     // one ballot per slot of a single compare (written straight to an SGPR
     // pair); forced slots, rare (reseeds, near-axis chords), balloted apart
@@ -1201,14 +1082,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (__ballot((forced >> j) & 1u)) spent |= 1u << j;
     }
     spent &= (2u << nb) - 1u;
-#ifdef SR_STATS_XCYL  // measurement only (tools/stats_frame.py --xcyl)
-    uint32_t trig = 0;  // slots some lane has spent itself (not look-ahead)
-#pragma unroll
-    for (int j = 0; j < NS; j++)
-        if (__ballot(!(T < e[j]) || ((forced >> j) & 1u))) trig |= 1u << j;
-    trig &= (2u << nb) - 1u;
-    if (!trig) SR_STAT(53, 1);  // an event no slot's budget asked for (the ball test's margins)
-#endif
     SR_PTB(20);
 #ifdef SR_PROF
     {
@@ -1293,21 +1166,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                 const float w = plane_window(st, A, B, ao, perr, dphi);
                 v = w > v ? w : v;  // NaN v stays NaN
             }
-            if (SR_CYL_PLANE && TY == SR_OBJECT_CYLINDER &&
-                !((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u)) {
-                // the frame's normal computed here: hoisted out of the slot
-                // loop it was held across it and spilled
-                f3 nv_ = nv, tv_ = tv;
-                asm volatile("" : "+v"(nv_.x), "+v"(nv_.y), "+v"(nv_.z), "+v"(tv_.x), "+v"(tv_.y), "+v"(tv_.z));
-                const float w = plane_window_x(st, nv_, tv_, B, SR_MU_QUADRATIC, st.qk) - perr;
-                v = w > v ? w : v;  // a NaN v stays NaN
-            }
-            if (SR_QPLANE && (TY == SR_OBJECT_SPHERE || TY == SR_OBJECT_BOX)) {
-                f3 nv_ = nv, tv_ = tv;
-                asm volatile("" : "+v"(nv_.x), "+v"(nv_.y), "+v"(nv_.z), "+v"(tv_.x), "+v"(tv_.y), "+v"(tv_.z));
-                const float w = plane_window_x(st, nv_, tv_, B, st.mu, 0.0f) - perr;
-                v = w > v ? w : v;
-            }
             if (TY != SR_OBJECT_PLANE && outward &&
                 outward_slot(st, TY == SR_OBJECT_CYLINDER &&
                                      ((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
@@ -1318,23 +1176,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             m = nmin(m, v);
             if (TY == SR_OBJECT_CYLINDER) {
                 const int k = __builtin_popcount(cyl & ((1u << (j - 1)) - 1u));
-#ifdef SR_STATS_XCYL
-                {  // could an orbital-plane exclusion of the cylinder have avoided this re-anchor?
-                    const f3 nrm_ = cross(A, B);
-                    const float nn = dot(nrm_, nrm_), hd = dot(ld3(st.bc), nrm_);
-                    const bool cmb = (bs.cm() >> k) & 1u;
-                    auto far = [&](float D) { return nn > 1.0e-6f * dot(A, A) * dot(B, B) && hd * hd > D * D * nn; };
-                    SR_STAT(44, 1);
-                    if (!__ballot(h)) SR_STAT(51, 1);
-                    SR_STAT(48, __popcll(__ballot(h)));
-                    SR_STAT(49, __popcll(__ballot(h && cmb)));
-                    SR_STAT(50, __popcll(__ballot(h && !far(3.6f))));
-                    if (!__ballot(h && (cmb || !far(3.6f)))) SR_STAT(45, 1);
-                    if (!__ballot(h && (cmb || !far(5.0f)))) SR_STAT(46, 1);
-                    if (!__ballot(h && (cmb || !far(8.0f)))) SR_STAT(47, 1);
-                    if (trig == (1u << j) && !__ballot(h && (cmb || !far(3.6f)))) SR_STAT(52, 1);
-                }
-#endif
                 const float vh = clearance_slab(st, B, a) - perr;
                 bs.E[(BS::L::SLAB0 + k) * SR_E_STRIDE] = vh;
                 mh = nmin(mh, vh);
@@ -1355,91 +1196,6 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     bs.setM(m);
     bs.setMh(mh);
     return reach;
-}
-
-// Side slots (SR_SIDE): at a budget event of the chord [A, B] (exact end
-// points within 4e-6 (rA + rB)) whose lanes have spent only planar slots
-// (mp < inf: the slab test of slot_reachable applies), at most SIDE of them,
-// each lane that spent one with both ends of its chord beyond that slot's
-// slab margin on the same side: the step is applied with no re-anchor and no
-// exact test (the chord cannot reach those slots, and every other budget
-// covers it: T < E[k], the event's own criterion), and the wave goes on with
-// those slots out of each such lane's ball. Per step it then tests the end
-// point X = (c, s) / u against each side slot's plane: y = (alpha c + beta s)
-// / u - g with alpha = nv . a1, beta = tv . a1, g = pos . a1, on the lane's
-// side sg beyond the margin m when sg alpha c + sg beta s - (sg g + m) u > 0.
-// Consecutive end points share their chords, so every chord of the stretch
-// has both ends beyond the slab and slot_reachable's planar test rejects it.
-// m is slot_reachable's margin for chords whose ends lie within Rb = 2.002
-// max(rA, rB) of the origin (S <= (sqrt(3) + 2) Rb + 1 covers |A|_1 + len +
-// 1, perr 8e-6 Rb), plus 1e-5 (Rb + |g| + 1) for the test's own float
-// evaluation (a few eps (2 r + |g| + m) in y) and alpha / beta's rounding;
-// lanes stop at u < 1 / (2 max(rA, rB)) (us). Lanes of the wave that did not
-// need a slot keep its budget in their ball (coefficients 0, 0, -1: always
-// true) unless they too are off its slab. Returns false, with nothing
-// changed, when the event cannot be replaced.
-template <class BS>
-__device__ __forceinline__ bool side_slots(const sr_dev_scene* __restrict__ sc, const BS& bs, f3 A, f3 B, float rA,
-                                           float rB, float cx, float cy, f3 nv, f3 tv, int& side_j) {
-    constexpr int NS = BS::NB + 1;
-    constexpr int SD = BS::L::SIDE;
-    const int nb = sc->num_budget;
-    const float ocx = bs.cx(), ocy = bs.cy();
-    const float dx = cx - ocx, dy = cy - ocy;
-    // the charge the event would make (budget_event: slot j covers the chord when T < E[j])
-    const float T = __builtin_fmaf(__builtin_amdgcn_sqrtf(dx * dx + dy * dy), 1.0101f,
-                                   3.0e-6f * (rB + fabsf(ocx) + fabsf(ocy)));
-    uint32_t sp = 0;  // wave-uniform: slots some lane has spent
-    float mq = INFINITY;  // this lane's ball: every budget but its side slots'
-#pragma unroll
-    for (int j = 0; j < NS; j++) {
-        if (j <= nb) {
-            const float e = bs.E[j * SR_E_STRIDE];
-            if (__ballot(!(T < e))) sp |= 1u << j;
-            else mq = nmin(mq, e);
-        }
-    }
-    if (sp == 0u || (sp & 1u) || __builtin_popcount(sp) > SD) return false;
-    const float Rm = 2.0f * fmaxf(rA, rB);
-    const float Rb = Rm * 1.001f;
-    const float perr = 8.0e-6f * Rb;
-    const float S = __builtin_fmaf(3.7321f, Rb, 1.0f) * 1.001f + perr;
-    int js[SD];
-    bool anyside = false;
-    uint32_t w = sp;
-    const int n = __builtin_popcount(sp);
-#pragma unroll
-    for (int k = 0; k < SD; k++) {
-        js[k] = 0;
-        if (k < n) {
-            const int j = __builtin_ctz(w);
-            w &= w - 1;
-            js[k] = j;
-            const sr_dev_slot sl = pin_slot(sc->slots[j - 1]);
-            if (!(sl.mp < INFINITY) || !(sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_DISK ||
-                                         sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_RECTANGLE))
-                return false;
-            const f3 pos = ld3(sl.pos), a1 = ld3(sl.a1);
-            const float g = dot(pos, a1);
-            const float m = (sl.mp + sl.mu * S) * 1.001f + perr + 1.0e-5f * (Rb + fabsf(g) + 1.0f);
-            const float yA = dot(A - pos, a1), yB = dot(B - pos, a1);
-            const bool side = (yA > m && yB > m) || (yA < -m && yB < -m);
-            const float e = bs.E[j * SR_E_STRIDE];
-            if (__ballot(!(T < e) && !side)) return false;
-            // (rows written before the wave's decision are unread while side_j is 0)
-            const float sg = yB > 0.0f ? 1.0f : -1.0f;
-            bs.st(BS::L::SP0 + 3 * k, side ? sg * dot(nv, a1) : 0.0f);
-            bs.st(BS::L::SP0 + 3 * k + 1, side ? sg * dot(tv, a1) : 0.0f);
-            bs.st(BS::L::SP0 + 3 * k + 2, side ? __builtin_fmaf(sg, g, m) : -1.0f);
-            if (!side) mq = nmin(mq, e);
-            anyside |= side;
-        }
-    }
-    bs.st(BS::L::QS, ball_q(mq, ocx, ocy));
-    bs.st(BS::L::US, anyside ? __builtin_amdgcn_rcpf(Rm) : 0.0f);
-    static_assert(SD == 1, "one side slot (side_j)");
-    side_j = js[0];
-    return true;
 }
 
 // The test rays (frag:760-803), visited right after the black hole.
@@ -2125,7 +1881,7 @@ __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 //   (u, u') += h6 ((fma(2, (k3, l3), fma(2, (k2, l2), (k1, l1)))) + (k4, l4))
 // in scalar binary32 instructions. The u and u' halves of a stage are the
 // same operations on different operands; as packed pairs (v_pk_mul_f32 /
-// v_pk_add_f32 / v_pk_fma_f32, SR_PACKED_RK4) they are half the instructions
+// v_pk_add_f32 / v_pk_fma_f32; round 3, removed since) they are half the instructions
 // but each takes the SIMD's issue for twice as long as a scalar one, and
 // need hazard s_nops: with six waves per SIMD the scalar form renders 2.9 %
 // more frames per second (one frame alone, latency bound, is 3.5 % slower;
@@ -2134,9 +1890,7 @@ __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 // non-subnormal q (the stage values here are never subnormal: DESIGN.md §4);
 // and 2 q is exact, so fma(2, q, a) is the rounding of a + 2 q, as the
 // reference's a + (2. * q).
-typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, float h6, float& un, float& dun) {
-#ifndef SR_PACKED_RK4
     const float k1 = du;
     const float l1 = ddu(u);
     const float k2 = du + l1 * hh;
@@ -2147,24 +1901,6 @@ __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, f
     const float l4 = ddu(u + k3 * h);
     un = u + h6 * (__builtin_fmaf(2.0f, k3, __builtin_fmaf(2.0f, k2, k1)) + k4);
     dun = du + h6 * (__builtin_fmaf(2.0f, l3, __builtin_fmaf(2.0f, l2, l1)) + l4);
-#else
-    // Each stage's (u_stage, k) pair is overwritten in place by (l, k) =
-    // (ddu(u_stage), k); the next stage reads it swapped (op_sel), so no
-    // pair is ever assembled with register moves.
-    const v2f s0 = {u, du};
-    const v2f H1 = {h, h}, H2 = {hh, hh}, two = {2.0f, 2.0f};
-    const v2f q1 = {du, ddu(u)};
-    v2f p1 = s0 + q1 * H2;  // (ua, k2)
-    p1.x = ddu(p1.x);       // (l2, k2)
-    v2f p2 = s0 + p1.yx * H2;  // (ub, k3)
-    p2.x = ddu(p2.x);          // (l3, k3)
-    v2f p3 = s0 + p2.yx * H1;  // (uc, k4)
-    p3.x = ddu(p3.x);          // (l4, k4)
-    const v2f hs = {h6, h6};
-    const v2f r = s0 + hs * (__builtin_elementwise_fma(two, p2.yx, __builtin_elementwise_fma(two, p1.yx, q1)) + p3.yx);
-    un = r.x;
-    dun = r.y;
-#endif
 }
 
 // The flat intersect of a ray that left the u_f sphere (frag:895-897,
@@ -2185,9 +1921,8 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 //
 // Lazy chords (CULL): the reference computes every chord exactly (two
 // divisions by u, a sqrt and three divisions by its length); here a step
-// only advances (u, du) and charges the clearance budgets an upper bound of
-// its chord length: with r = 1/u the chord of two orbit points is
-// sqrt((rB - rA)^2 + rA rB g) (g from the step table) up to float rounding.
+// only advances (u, du) and tests its end point against the lane's ball
+// (ball_q: every budget covers the chords whose ends lie in it).
 // When a budget is spent (or the chord may be near-parallel to a budgeted
 // cylinder) the wave runs a budget event on the approximate chord
 // (point_near); only when a slot may be reached is the exact chord
@@ -2217,7 +1952,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f);
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -2265,9 +2000,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         im = i - 1;
     };
     bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
-    // side slots (SR_SIDE, wave-uniform): how many, and which
-    constexpr bool SIDE = CULL && BS::L::SIDE > 0;
-    int side_j = 0;  // the side slot (side_slots; 0: none - slot 0, the hole, is never one)
     int i = r.i;
 #ifdef SR_STATS
     int last_ev = i;
@@ -2287,12 +2019,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // every reseed happens)
         SR_PT(21);
         if (__ballot(r.u < fr.u_f)) {
-            side_j = 0;  // a new orbital frame: the side tests' coefficients are the old frame's
             if (r.u < fr.u_f) {
                 r.i = i;
                 r.steps = sbase + i + 1;
                 settle_prev(i);
-#if SR_BALL
                 // the new orbital plane has its own coordinates: charge the
                 // displacement from the old centre to the chord start r.ro
                 // here, the new chord at the forced event (reseeded)
@@ -2302,7 +2032,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     bs.setT(__builtin_fmaf(len(r.ro - (r.nv * ocx + r.tv * ocy)), 1.0101f,
                                            3.0e-6f * (fabsf(ocx) + fabsf(ocy) + 1.0f)));
                 }
-#endif
                 float lam;
                 if (!sphere_lambda_r2(r.ro, r.rd, F3(0.0f, 0.0f, 0.0f), fr.uf_radius2, -1.0f, lam))
                     return flat_misses(sc, r.ro, r.rd) ? ST_BG : ST_FLAT;
@@ -2312,32 +2041,29 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
                 r.u = 1.0f / len(q);
                 r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-                if (CULL) budget_frame(sc, bs, r.nv, r.tv);
+                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s);
                 force = true;  // the chord starts at the exact r.ro
             }
             SR_PT(1);
         }
-        // ---- fast loop: RK4, the chord-length bound and one compare per
-        // step, the same instructions on every lane and wave-uniform exits
-        // only. The wave leaves with step i computed but not applied when
-        // some lane needs attention: a budget event (Tn >= its limit; the
-        // limit is -inf while every chord is tested or this lane's chord is
-        // forced), an exit (u < 0) or a reseed at the next step (u < u_f).
+        // ---- fast loop: RK4, the ball test of the step's end point and
+        // the u compares per step, the same instructions on every lane and
+        // wave-uniform exits only. The wave leaves with step i computed but
+        // not applied when some lane needs attention: a budget event (the
+        // end point left its ball, ball_q; an empty ball while every chord is
+        // tested or this lane's chord is forced), an exit (u < 0) or a reseed
+        // at the next step (u < u_f).
         // Only numbers leave the loop (lane-mask booleans carried out of it
         // cost exec-mask bookkeeping on every step).
         const float bm = bs.m();
         const float lim0 = (every || force) ? -INFINITY : bm;
         const float uhi = bs.uhi();  // u > uhi: the chord left the black hole's u window
-        // u < ulo: a reseed or exit at the next step, or the inner window's
-        // end (with a side slot: or the radius bound of its margin)
-        const float ulo = (SIDE && side_j) ? fmaxf(BS::ulo_of(uhi, fr.u_f), bs.us()) : BS::ulo_of(uhi, fr.u_f);
-#if SR_BALL
+        // u < ulo: a reseed or exit at the next step, or the inner window's end
+        const float ulo = BS::ulo_of(uhi, fr.u_f);
         const float bcx = CULL ? bs.cx() : 0.0f, bcy = CULL ? bs.cy() : 0.0f;
         const float bn = -2.0f * bcx, bt = -2.0f * bcy;
-        // (with a side slot: the ball without it, side_slots)
-        const float q0 = (!CULL || every || force) ? INFINITY : (SIDE && side_j) ? bs.qs() : ball_q(bm, bcx, bcy);
+        const float q0 = (!CULL || every || force) ? INFINITY : ball_q(bm, bcx, bcy);
         float vb;  // the step's ball test (< 0: inside)
-#endif
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
         // (bs.cm changes only at reseeds, outside the fast loop)
         const uint32_t bcm = CULL ? bs.cm() : 0u;
@@ -2345,17 +2071,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
         const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
-#if SR_CTABLE
-        const float* fp = reinterpret_cast<const float*>(tbl + 2 * (N + 4)) + 5 * i;  // compact entry of step i
-        // entry of step i from the compact table: (e, e1) with e1.y = 0.5 step_size
-        auto ldcompact = [&](float4& ee, float4& ee1) {
-            const sr_v8f_a4 v = *(const sr_cf8a*)fp;
-            ee = make_float4(v[0], v[1], v[2], v[3]);
-            ee1 = make_float4(0.0f, v[4], 0.0f, 0.0f);
-        };
-#endif
         float4 e;
-        float un, dun, rB, Tn, lim;
+        float un, dun, rB;
         uint32_t par;
         // Three versions of the loop: without a lane whose orbital plane nearly
         // contains a budgeted cylinder's axis (the usual case, CMV 0) the
@@ -2370,48 +2087,25 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // 2 SR_BUDGET_DPMIN, direction known to 0.004) and the margin's
         // (|d_perp|^2 >= SR_BUDGET_DPMIN). The exit step's chord is tested
         // again in the slow path (its end may lie beyond the window).
-        auto fast = [&](auto cm_tag, auto sd_tag) {
+        auto fast = [&](auto cm_tag) {
             constexpr int CMV = decltype(cm_tag)::value;
             constexpr bool CM = CMV != 0;
-            constexpr int NSD = decltype(sd_tag)::value;  // side slots tested per step (CMV 0 only)
-            static_assert(NSD == 0 || CMV == 0, "side slots with the cylinder-plane loop");
-            lim = lim0;
             par = 0;
             float4 e1;
-#if SR_CTABLE
-            ldcompact(e, e1);
-#else
             e = ldc(tp);
             e1 = ldc(tp + 1);
-#endif
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs<NC> cd = CM ? cyl_dirs(sc, bs) : CylDirs<NC>{};
-#if SR_BALL
             const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bm, bs.mh()), bcx, bcy)) : q0;
-#endif
             // the LDS reads land before the loop: a wait for them inside it
             // would also wait for the step table's prefetch (one counter)
-            // side slots: the ball without them, the lanes' radius bound and
-            // per side slot (sa, sb, sc): the end point (cos phi, sin phi) / u
-            // is off the slot's slab on the lane's side when sa cos phi + sb
-            // sin phi - sc u > 0 (side_slots)
-            float sa[2] = {0.0f, 0.0f}, sb[2] = {0.0f, 0.0f}, scc[2] = {0.0f, 0.0f};
-            if (NSD > 0) {
-#pragma unroll
-                for (int s = 0; s < NSD; s++) {
-                    sa[s] = bs.sp(s, 0);
-                    sb[s] = bs.sp(s, 1);
-                    scc[s] = bs.sp(s, 2);
-                }
-            }
-            if (CM || NSD > 0) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             float qit = q0;  // CMV 2: the iteration's ball
             // Step i from entry (e, e1): RK4, the chord-length bound and the
             // exit test; true when some lane needs attention (the step is then
             // computed but not applied). k: the step's place in the iteration.
             auto compute = [&](int k) -> bool {
                 rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
-#if SR_BALL
                 // the end point against the ball (ball_q): a multiply and three FMAs
                 float q = q0;
                 if (CULL && CMV == 1) {
@@ -2434,50 +2128,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
                 if (CM) SR_STAT(31, 1);  // wave-steps of the cylinder-plane fast loop
 #endif
-#ifdef SR_STATS_PLANE
-                if (NSD > 0) SR_STAT(54, 1);  // wave-steps with side slots
-#endif
-                if (NSD > 0) {
-                    bool sf = false;
-#pragma unroll
-                    for (int s = 0; s < NSD; s++)
-                        sf |= !(__builtin_fmaf(sa[s], e.z, __builtin_fmaf(sb[s], e.w, -scc[s] * un)) > 0.0f);
-                    return __ballot(!(vb < 0.0f) || un < ulo || un > uhi || sf);
-                }
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
-#endif
-                rB = __builtin_amdgcn_rcpf(un);
-                Tn = bs.T();
-                if (CULL) {
-                    // chord length bound: sqrt(dr^2 + rA rB g) K_i, K_i covering the 1e-4
-                    // relative allowance, point_err (<= 4e-6 (2 / sqrt(g) + 1) sqrt(...):
-                    // sr_api.cpp ensure_table) and the path slack (bounds, not reference
-                    // arithmetic: FMA allowed)
-                    const float dr = rB - rA;
-                    const float sq = __builtin_amdgcn_sqrtf(__builtin_fmaf(dr, dr, (rA * rB) * e1.x));
-                    Tn = __builtin_fmaf(sq, e1.z, Tn);
-                    if (CM) {
-                        par = chord_parallel(bcm, cd, rB * e.z - rA * pc.x, rB * e.w - rA * pc.y, point_err(rA, rB));
-                        lim = par ? nmin(lim0, bs.mh()) : lim0;
-                    }
-                }
-                SR_STAT(0, 1);
-                SR_STAT(13, __popcll(__ballot(1)));
-                // un < u_f covers un < 0 (frag:921-922: get_bg with the previous chord);
-                // un > uhi: the chord left the black hole's u window
-                return __ballot(!(Tn < lim) || un < fr.u_f || un > uhi);
             };
             // apply step i and move to entry (en, en1) of step i + 1
             auto apply = [&](float4 en, float4 en1) -> bool {
-                if (!SR_BALL) bs.setT(Tn);
                 r.u = un;
                 r.du = dun;
-                if (!SR_BALL || CMV == 1) rA = rB;
-#if SR_CTABLE
-                fp += 5;
-#else
+                if (CMV == 1) rA = rB;
                 tp += 2;
-#endif
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
                 e1 = en1;
@@ -2491,42 +2149,21 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // they are issued (sunk to their first use, they would be waited
             // at once).
             for (;;) {
-#if SR_CTABLE
-                static_assert(FU <= 3, "one 16-dword load holds three compact entries");
-                const sr_v16f_a4 nv = *(const sr_cf16a*)(fp + 5);  // steps i + 1 .. i + 3
-#else
                 float4 nx[2 * FU];
 #pragma unroll
                 for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
-#endif
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     if (compute(k)) {
-#if SR_CTABLE
-                        asm volatile("; keep %0" ::"s"(nv[5 * FU - 1]));
-#else
 #pragma unroll
                         for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
-#endif
                         leave = true;
                     } else {
-#if SR_CTABLE
-                        leave = apply(make_float4(nv[5 * k], nv[5 * k + 1], nv[5 * k + 2], nv[5 * k + 3]),
-                                      make_float4(0.0f, nv[5 * k + 4], 0.0f, 0.0f));
-#else
                         leave = apply(nx[2 * k], nx[2 * k + 1]);
-#endif
                     }
                 }
-#if SR_CTABLE
-                // the load's unused dwords: without a use the compiler reuses
-                // their registers while the load is in flight, which waits
-                // for the load at the top of the iteration
-#pragma unroll
-                for (int j = 5 * FU; j < 16; j++) asm volatile("; keep %0" ::"s"(nv[j]));
-#endif
                 if (leave) break;
             }
         };
@@ -2540,20 +2177,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // coast: u stays finite.
         auto coast = [&]() {
             float4 e1;
-#if SR_CTABLE
-            ldcompact(e, e1);
-#else
             e = ldc(tp);
             e1 = ldc(tp + 1);
-#endif
             for (;;) {
-#if SR_CTABLE
-                const sr_v16f_a4 nv = *(const sr_cf16a*)(fp + 5);  // steps i + 1 .. i + 3
-#else
                 float4 nx[2 * FU];
 #pragma unroll
                 for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
-#endif
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
@@ -2563,43 +2192,25 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
                     if (__ballot(un < ulo || un > uhi)) {
-#if SR_CTABLE
-                        asm volatile("; keep %0" ::"s"(nv[5 * FU - 1]));
-#else
 #pragma unroll
                         for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
-#endif
                         leave = true;
                     } else {
                         r.u = un;
                         r.du = dun;
-#if SR_CTABLE
-                        fp += 5;
-                        e = make_float4(nv[5 * k], nv[5 * k + 1], nv[5 * k + 2], nv[5 * k + 3]);
-                        e1 = make_float4(0.0f, nv[5 * k + 4], 0.0f, 0.0f);
-#else
                         tp += 2;
                         e = nx[2 * k];
                         e1 = nx[2 * k + 1];
-#endif
                         leave = ++i >= N;
                     }
                 }
-#if SR_CTABLE
-#pragma unroll
-                for (int j = 5 * FU; j < 16; j++) asm volatile("; keep %0" ::"s"(nv[j]));  // as in fast()
-#endif
                 if (leave) break;
             }
             // the state the full loop leaves: step i's radius, no charge (every budget is +inf)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
-            Tn = bs.T();
-            lim = lim0;
             par = 0;
-#if SR_BALL
             vb = -1.0f;  // inside every (infinite) budget
-#endif
         };
         // The fast loop does not carry `up` (u after step i - 2): the copy
         // cost a register move per step in its rotation (42.3 -> 41.7 VALU
@@ -2627,18 +2238,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
-        if constexpr (SIDE) {
-            if (side_j) fast(I0{}, I1{});
-            else if (cm_iter) fast(I2{}, I0{});
-            else if (any_cm) fast(I1{}, I0{});
-            else if (SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
-            else fast(I0{}, I0{});
-        } else {
-            if (cm_iter) fast(I2{}, I0{});
-            else if (any_cm) fast(I1{}, I0{});
-            else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
-            else fast(I0{}, I0{});
-        }
+        if (cm_iter) fast(I2{});
+        else if (any_cm) fast(I1{});
+        else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
+        else fast(I0{});
         SR_PT(0);
         if (i >= N) {
             up = recover_up(N);
@@ -2657,31 +2260,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         }
         // the chord left the black hole's u window (or the inner one outward)
         const bool bhx = un > uhi || (un < SR_BH_ULO2 && uhi == SR_BH_U2);
-#if SR_BALL
-        // side slot: lanes whose chord end reached its slab (or passed the
-        // radius its margin was sized for) need an event (budget_event
-        // forces the slot's re-anchor for them)
-        bool sfail = false;
-        if constexpr (SIDE) {
-            static_assert(BS::L::SIDE == 1, "one side slot");
-            if (side_j) {
-                const float w = __builtin_fmaf(bs.sp(0, 0), e.z, __builtin_fmaf(bs.sp(0, 1), e.w, -bs.sp(0, 2) * un));
-                sfail = !(w > 0.0f) || un < bs.us();
-            }
-        }
-        const bool event = !(vb < 0.0f) || bhx || sfail;
+        // a chord ending beyond 2 / u_f, which the orbital-plane exclusions do
+        // not cover (budget_frame): an event that forces them (budget_event)
+        const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f);
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
         }
-#else
-        const bool event = !(Tn < lim) || bhx;
-        // slots about to run out re-anchor at this event too (within SR_AHEAD
-        // of this chord's length plus SR_AHEAD_T of the path since the last
-        // event): fewer events, each re-anchoring more
-        const float ahead = SR_AHEAD * (Tn - bs.T()) + SR_AHEAD_T * Tn;
-        bs.setT(Tn);
-#endif
         up = r.u;
         r.u = un;
         r.du = dun;
@@ -2693,31 +2278,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             if (!__ballot(event)) break;
             uint32_t reach = 0xffffffffu;
             const f2 p1 = phi_cs(i - 1);
-            int sjx = 0;
             if (CULL) {
                 // the approximate chord (exact start when materialised)
                 const bool exact_start = im == i - 1;
                 const f3 Ap = exact_start ? r.ro : point_near(r, rAold, p1.x, p1.y);
                 const f3 Bp = point_near(r, rB, e.z, e.w);
                 const float pe = point_err(exact_start ? 0.0f : rAold, rB);
-#if SR_BALL
-                if constexpr (SIDE) {
-                    sjx = side_j;  // the side slot this event may force
-                    side_j = 0;
-                    // only planar slots spent, chords off their slabs: no event (side_slots)
-                    if (!every && !any_cm && !__ballot(reseeded || bhx || sfail) &&
-                        side_slots(sc, bs, Ap, Bp, rAold, rB, rB * e.z, rB * e.w, r.nv, r.tv, side_j)) {
-#ifdef SR_STATS_PLANE
-                        SR_STAT(55, 1);
-#endif
-                        break;
-                    }
-#ifdef SR_STATS_PLANE
-                    if (__ballot(sfail)) SR_STAT(57, 1);
-#endif
-                }
-#endif
-#if SR_BALL
                 // the displacement from the ball's centre to the step's end
                 // point Bp, which becomes the centre: bs.T bounds 1.01 x the
                 // distance between the centres' embeddings and between the
@@ -2743,12 +2309,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     ahead = SR_AHEAD * SR_PATH_SLACK * cl + SR_AHEAD_T * T;
                     bs.setC(cx, cy);
                 }
-#else
-                if (reseeded) {  // new frame: the step's bound used the old radius; charge the chord itself
-                    const f3 dv = Bp - Ap;
-                    bs.setT(bs.T() + (__builtin_amdgcn_sqrtf(dot(dv, dv)) * 1.0001f + pe) * SR_PATH_SLACK);
-                }
-#endif
                 SR_STAT(1, 1);
 #ifdef SR_STATS
                 r.ev++;
@@ -2758,50 +2318,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
                     const int nl = __popcll(__ballot(event));
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
-#ifdef SR_STATS_PLANE  // measurement only (tools/stats_frame.py --plane): counters 44..53
-                    {
-                        // a triggering lane is "plane-avoidable" when every slot it has
-                        // spent is planar and this chord stays off that slot's
-                        // acceptance slab (slot_reachable's planar test): a per-step
-                        // plane test would not have stopped it
-                        const float T = bs.T();
-                        const bool trig = event;
-                        bool avoid = trig && !bhx && !reseeded && T < bs.E[0];
-                        bool anyspent = false, anyplanar = false;
-                        const f3 dv = Bp - Ap;
-                        const float ln = __builtin_amdgcn_sqrtf(dot(dv, dv));
-                        const float S = ((fabsf(Ap.x) + fabsf(Ap.y) + fabsf(Ap.z)) + ln + 1.0f) * 1.001f + pe;
-                        for (int j = 1; j <= sc->num_budget && j <= NB; j++) {
-                            if (T < bs.E[j * SR_E_STRIDE]) continue;
-                            anyspent = true;
-                            const sr_dev_slot& sl = sc->slots[j - 1];
-                            const bool planar = sl.mp < INFINITY &&
-                                                (sl.type == SR_OBJECT_PLANE || sl.type == SR_OBJECT_DISK ||
-                                                 sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_RECTANGLE);
-                            if (!planar) { avoid = false; continue; }
-                            anyplanar = true;
-                            const float mm = (sl.mp + sl.mu * S) * 1.001f + pe;
-                            const f3 pos = ld3(sl.pos), a1 = ld3(sl.a1);
-                            const float yA = dot(Ap - pos, a1), yB = dot(Bp - pos, a1);
-                            if (!((yA > mm && yB > mm) || (yA < -mm && yB < -mm))) avoid = false;
-                        }
-                        avoid = avoid && anyspent;
-                        SR_STAT(44, 1);
-                        SR_STAT(47, __popcll(__ballot(trig)));
-                        SR_STAT(48, __popcll(__ballot(avoid)));
-                        SR_STAT(49, __popcll(__ballot(trig && anyplanar)));
-                        SR_STAT(50, __popcll(__ballot(trig && !anyspent && !bhx && T < bs.E[0])));
-                        if (!__ballot(trig && !avoid)) {
-                            SR_STAT(45, 1);
-                            if (iv <= 1) SR_STAT(46, 1);
-                        }
-                        // every triggering lane avoidable or without a spent slot (the ball's margins)
-                        if (!__ballot(trig && !avoid && (anyspent || bhx || !(T < bs.E[0])))) SR_STAT(51, 1);
-                        if (__ballot(avoid)) SR_STAT(52, 1);
-                        if (iv <= 1) SR_STAT(53, 1);
-                    }
-#endif
-#if SR_BALL && !defined(SR_STATS_XCYL) && !defined(SR_STATS_PLANE)  // (SR_STATS_XCYL: counters 44..53 in budget_event instead)
                     if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
                     SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
                     SR_STAT(46, __popcll(__ballot(bhx)));
@@ -2824,7 +2340,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                         }
                     }
                     SR_STAT(54, any_cm);
-#endif
                 }
 #endif
                 // sr_wave_costs: the wave's event count (one lane, its own LDS word)
@@ -2869,8 +2384,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 }
 #endif
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                                         fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, r.nv, r.tv,
-                                         cm_iter, sjx, e.z, e.w, r.u);
+                                     fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
+                                     fr.u_f);
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);

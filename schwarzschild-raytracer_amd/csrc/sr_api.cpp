@@ -351,43 +351,17 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const 
     // frag:860, 914-915, 925: the angle sequence depends only on the step index
     const float max_angle = 2.0f * (float)max_revs * kPi;
     // entry i = two float4: {step_size, step_size / 6, cos phi, sin phi} and
-    // {g, 0, 0, 0} with g = 2 (sqrt(n_(i-1) n_i) - p_i) for the float unit
-    // vectors (cos, sin) of steps i - 1 and i (n = squared norm, p = their dot;
-    // step -1 is phi = 0): the squared chord of two orbit points at radii
-    // r1, r2 is (r2 - r1)^2 + r1 r2 g up to float rounding (kernel chord
-    // bound). The second float4 is {g, 0.5 step_size, K, 0}: 0.5 step_size for
-    // RK4 (exact), and K the chord bound's factor: a chord's float end points
-    // lie within 4e-6 (r1 + r2) of the ideal ones, and r1 + r2 <= (2 / sqrt(g)
-    // + 1) sqrt((r2 - r1)^2 + r1 r2 g) (min(r1, r2) <= sqrt(r1 r2)), so
-    // K = (1.0001 + 4.01e-6 (2.001 / sqrt(g) + 1)) x path slack 1.01, rounded
-    // up, covers both. Four padding entries (the step loop loads up to four steps ahead).
-    // Then the fast loop's compact table (geodesic.hip SR_CTABLE): 5 floats
-    // per step {step_size, step_size / 6, cos phi, sin phi, 0.5 step_size},
-    // the same values, plus padding for a 16-dword load three steps ahead
-    const size_t main4 = 2 * ((size_t)max_steps + 4);
-    const size_t compact4 = (5 * ((size_t)max_steps + 4) + 3) / 4 + 1;
-    std::vector<float4> h(main4 + compact4, make_float4(0.f, 0.f, 0.f, 0.f));
-    float* ct = reinterpret_cast<float*>(h.data() + main4);
+    // {0, 0.5 step_size, 0, 0} (0.5 step_size for RK4, exact; the fast loop
+    // loads both with scalar loads of a 32-byte entry). Four padding entries:
+    // the step loop loads up to four steps ahead.
+    std::vector<float4> h(2 * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
-    double c1 = 1.0, s1 = 0.0;
     for (int i = 0; i < max_steps; i++) {
         float step = (max_angle - phi) / (float)(max_steps - i);
         phi += step;
         const float c = (float)std::cos((double)phi), sn = (float)std::sin((double)phi);
         h[2 * (size_t)i] = make_float4(step, step / 6.0f, c, sn);
-        const double n1 = c1 * c1 + s1 * s1, n2 = (double)c * c + (double)sn * sn, pr = c1 * c + s1 * sn;
-        double g = 2.0 * (std::sqrt(n1 * n2) - pr);
-        g = g > 0.0 ? g * (1.0 + 1e-6) + 1e-30 : 1e-30;  // rounded up
-        const double K = (1.0001 + 4.01e-6 * (2.001 / std::sqrt(g) + 1.0)) * 1.01 * (1.0 + 1e-6);
-        h[2 * (size_t)i + 1] = make_float4((float)g, 0.5f * step, std::nextafter((float)K, INFINITY), 0.f);
-        float* q = ct + 5 * (size_t)i;
-        q[0] = step;
-        q[1] = step / 6.0f;
-        q[2] = c;
-        q[3] = sn;
-        q[4] = 0.5f * step;
-        c1 = c;
-        s1 = sn;
+        h[2 * (size_t)i + 1] = make_float4(0.f, 0.5f * step, 0.f, 0.f);
     }
     evict_tables(ctx);
     Table& t = ctx->tables[key];
@@ -635,6 +609,14 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     fr.u_f = p->u_f;
     fr.uf_radius = 1.0f / p->u_f;
     fr.uf_radius2 = fr.uf_radius * fr.uf_radius;  // binary32, as the kernel would compute it
+    {
+        // chords start within R = 1 / u_f and end within 2 R, or are forced
+        // (geodesic.hip budget_frame): S <= (sqrt 3 + 3) R + 1
+        const double R = p->u_f > 0.0f ? 1.0 / (double)p->u_f : INFINITY;
+        // (x 1.005: the chord ends' 4e-7 r off the orbital plane, as mu >= SR_MU_PLANAR)
+        const double S = ((std::sqrt(3.0) + 3.0) * R * (1.0 + 1e-5) + 1.0) * 1.001 * 1.005;
+        fr.xplane_s = S < 1.0e30 ? std::nextafter((float)S, INFINITY) : INFINITY;
+    }
     fr.percent_black = p->percent_black;
     fr.curved_percentage = p->curved_percentage;
     fr.max_steps = p->max_steps;

@@ -701,3 +701,25 @@ def test_zz_diag_counters_zero(gpu):
     (the step loop's classification is exact where it claims), and no
     stream-ordered free failed."""
     assert gpu.diag_counters() == {"hit_not_opaque": 0, "free_errors": 0}
+
+
+@pytest.mark.parametrize("u_f", [1.0e-4, 0.01, 0.05])
+def test_objects_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f):
+    """The orbital-plane exclusion (geodesic.hip budget_frame) with its
+    bound S_max = (sqrt 3 + 3) / u_f + 1 (sr_dev_frame.xplane_s): a sphere and
+    a box on the line through the camera and the hole lie near the pencil of
+    orbital planes through that line, at the exclusion's margin, for small and
+    large u_f (chords up to r = 2e4 with u_f = 1e-4, where the bound is
+    effectively off; the near-radial escapes to u < u_f / 2 force the
+    excluded slots). Whole 160x90 frames, bit-exact with step counts."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    for k, v in enumerate((0.05, 1.02, 7.3)):
+        scene.spheres[0].transform.pos[k] = v
+    for k, v in enumerate((-0.4, -1.1, -8.2)):
+        scene.boxes[0].transform.pos[k] = v
+    cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
+    params = abi.default_params(max_steps=1200, percent_black=-1.0, u_f=u_f)
+    g = gpu_debug(gpu, scene, cam, params, 160, 90)
+    o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
+    print(compare(g, o, f"objects near orbital planes, u_f {u_f}"))

@@ -22,8 +22,6 @@ def main():
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
     ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080], help="render only rows [a, b) (waves alone on the chip)")
-    ap.add_argument("--xcyl", action="store_true", help="an SR_STATS_XCYL build (counters 44..53)")
-    ap.add_argument("--plane", action="store_true", help="an SR_STATS_PLANE build (counters 44..53)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -80,21 +78,6 @@ def main():
              "interval1_triggered", "interval1_reseeded", "interval1_budget_below_0.05", "interval1_cm_events",
              "cm_events"])}
         out["interval1_small_budget_lanes_by_slot"] = [int(hi[23 + j]) for j in range(9)]
-        if args.xcyl:  # an SR_STATS_XCYL build: counters 44..53 hold the cylinder exclusion probe
-            for k in ("event_lanes", "events_bh_window_only"):
-                out.pop(k, None)
-            out["xcyl"] = dict(zip(["reanchors", "avoidable_3.6", "avoidable_5", "avoidable_8", "spent_lanes",
-                                    "spent_lanes_cm", "spent_lanes_near_3.6", "lookahead_only",
-                                    "events_avoidable_3.6", "events_no_slot_spent"], [int(hi[12 + k]) for k in range(10)]))
-        if args.plane:  # an SR_STATS_PLANE build: counters 44..53 hold the planar-slab probe
-            for k in ("event_lanes", "events_bh_window_only"):
-                out.pop(k, None)
-            out["plane"] = dict(zip(["events", "events_avoidable", "events_avoidable_interval1", "trig_lanes",
-                                     "avoidable_lanes", "planar_spent_lanes", "no_slot_spent_lanes",
-                                     "events_avoidable_or_margin", "events_with_avoidable_lane",
-                                     "events_interval1"], [int(hi[12 + k]) for k in range(10)]))
-            out["side"] = dict(zip(["wave_steps", "transitions", "transitions_2", "side_fail_events"],
-                                   [int(hi[22 + k]) for k in range(4)]))
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
 
