@@ -684,6 +684,9 @@ def main():
                 "launches_in_flight": F,
                 "frames_per_launch": B,
                 "frames_in_flight": F * B,
+                # the timed window's launches (frames each): a window that is
+                # not a multiple of B ends with a shorter launch
+                "launch_sizes": [min(B, args.steps - f) for f in range(0, args.steps, B)],
                 "split_tiles": args.split,
                 "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                 "frame_latency_ms": round(latency_ms, 4),
@@ -915,7 +918,11 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
         "frames_per_launch": B,
         "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
                         "resume": round(resume_ms, 4)},
-        "steps_per_launch": sigma_steps_mine,
+        # this rank's executed ray-steps of one frame (the debug render of the
+        # first camera), and of one launch of B frames (static camera: B times
+        # that; a flyby's frames differ, so none)
+        "steps_per_frame": sigma_steps_mine,
+        "steps_per_launch": sigma_steps_mine * B if args.camera == "static" else None,
         "mean_steps_per_pixel": round(sigma_steps_frame / (W * H), 2),
         "pmc_source": None if not pmc else pmc.get("source"),
         # the un-culled reference loop (360 FLOP per step) and the

@@ -145,3 +145,32 @@ def test_spawn_ranks_env_and_status(tmp_path):
         assert bench.spawn_ranks(2, ["7", "1"], grace_s=5) == 7
     finally:
         bench.__file__ = old
+
+
+def test_roofline_steps_per_frame_and_launch():
+    """roofline.steps_per_frame is one frame's executed ray-steps of the
+    rank's rows, and steps_per_frame x frames_per_launch the launch's (a
+    static camera: B equal frames), checked against the oracle's step map of a
+    small config rendered B times."""
+    import argparse
+
+    import numpy as np
+
+    import bench
+    import srpkg
+
+    pkg, oracle = srpkg.load_package(), srpkg.load_oracle()
+    sc, abi = pkg.scenes, pkg.abi
+    W, H, N, B = 48, 32, 300, 3
+    scene, cam = sc.scene_default(textured=False), abi.default_camera()
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    tex = oracle.TextureSet(sc.skybox(64, 32), sc.default_texture_array()[0])
+    launch_steps = sum(int(oracle.render(scene, cam, params, W, H, tex)[2].astype(np.int64).sum()) for _ in range(B))
+    frame_steps = launch_steps // B
+    args = argparse.Namespace(pmc_json="/nonexistent", traffic_json="/nonexistent", camera="static")
+    rf = bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None, None)
+    assert rf["steps_per_frame"] == frame_steps and rf["frames_per_launch"] == B
+    assert rf["steps_per_frame"] * rf["frames_per_launch"] == rf["steps_per_launch"] == launch_steps
+    args.camera = "flyby"
+    assert bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None,
+                               None)["steps_per_launch"] is None
