@@ -147,6 +147,12 @@ def parse():
     ap.add_argument("--skybox", choices=["auto", "2k", "8k"], default="auto",
                     help="BACKGROUND_TEXTURE_QUALITY (src/main.cpp:57-63); auto: 8k for the 8k still, else 2k")
     ap.add_argument("--no-cull", action="store_true", help="exhaustive per-object tests (reference loop)")
+    ap.add_argument("--scene", choices=["default", "stress"], default="default",
+                    help="default: the app's scene (src/main.cpp:222-268); stress: every capacity of the uniform "
+                         "block filled (scenes.scene_stress: 3 of each primitive, 10 materials, 4 lights)")
+    ap.add_argument("--test-ray", choices=["off", "on"], default="off",
+                    help="the press-R overlay (frag:760-803, src/main.cpp:375-391): a 1000-point test-ray polyline "
+                         "drawn into every frame (scenes.test_ray_overlay)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="launches in flight per GPU, each on its own context and stream (0: 3 for batched "
                          "launches, 4 for single frames)")
@@ -316,7 +322,8 @@ def main():
             dist.init_process_group("gloo")
 
     # ---- inputs resident in HBM ---------------------------------------------------
-    scene = sc.scene_default(textured=True)
+    scene = sc.scene_stress() if args.scene == "stress" else sc.scene_default(textured=True)
+    test_ray = sc.test_ray_overlay() if args.test_ray == "on" else None
     params = abi.default_params(max_steps=N, percent_black=args.percent_black, raytrace_type=MODES[args.mode],
                                 curved_percentage=args.curved_percentage)
     quality = args.skybox if args.skybox != "auto" else ("8k" if (W, H) == WORKLOADS["8k"][:2] else "2k")
@@ -345,12 +352,19 @@ def main():
     D = pkg.dist
     gloo = distributed and args.dist_backend == "gloo"
     ctxs = []
-    for k in range(F):
+    def new_renderer():
+        """a context with the run's inputs resident (scene, textures, test ray)"""
         rk = pkg.Renderer(dev.index)
         rk.set_scene(scene)
         rk.set_background(skybox)
         rk.set_texture_array(arr)
         rk.set_culling(not args.no_cull)
+        if test_ray is not None:
+            rk.set_test_ray(test_ray)
+        return rk
+
+    for k in range(F):
+        rk = new_renderer()
         rk.set_split(split[0], split[1], split[2])
         tile_k = torch.zeros((B, D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
         host_k = torch.zeros(tuple(tile_k.shape), dtype=torch.uint8).pin_memory() if gloo else None
@@ -480,10 +494,7 @@ def main():
         rp["every"] = args.reprice if args.reprice >= 0 else (F if args.camera == "flyby" else 0)
         sched[0] = D.ListSchedule(lists[0], F, rp["every"], B)
         if rp["every"] and rank == 0:
-            rp["pricer"] = pkg.Renderer(dev.index)
-            rp["pricer"].set_scene(scene)
-            rp["pricer"].set_background(skybox)
-            rp["pricer"].set_texture_array(arr)
+            rp["pricer"] = new_renderer()
             rp["stream"] = torch.cuda.Stream(dev)
     else:
         rows_mine = D.rows_of(rank, world, H, BLOCK_ROWS)
@@ -551,8 +562,8 @@ def main():
     # single-frame launches with 4 in flight (B = 1, F = 4).
     single = None
     if world == 1 and args.single_frame == "on":
-        single = single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, args.single_split,
-                               args.no_cull, render, warm, restore=split)
+        single = single_frames(new_renderer, ctxs, cams, params, W, H, dev, args.single_split, render, warm,
+                               restore=split)
 
     # the reference's loop: one un-culled frame against one culled frame, alone
     speedup_ref = None
@@ -613,11 +624,7 @@ def main():
     # slowest waves' latency without contention.
     critical = None
     if rank == 0 and world == 1 and args.critical_path == "on":
-        rb = pkg.Renderer(dev.index)
-        rb.set_scene(scene)
-        rb.set_background(skybox)
-        rb.set_texture_array(arr)
-        rb.set_culling(not args.no_cull)
+        rb = new_renderer()
 
         def band_time(band, reps):
             for _ in range(2):
@@ -663,11 +670,15 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic: default scene of src/main.cpp:222-268, {tex_desc}",
+            "data": ("synthetic: " + ("the max-capacity scene (scenes.scene_stress: 21 objects, 10 materials, 4 lights)"
+                                      if args.scene == "stress" else "default scene of src/main.cpp:222-268")
+                     + (", the press-R overlay (scenes.test_ray_overlay, 1000 points)" if test_ray is not None else "")
+                     + f", {tex_desc}"),
             "config": {
                 "workload": (f"{W}x{H} {args.mode}-mode frame"
                              + (f" (curved_percentage {args.curved_percentage})" if args.mode.startswith("half") else "")
-                             + f", {N} geodesic steps, default scene, percent_black "
+                             + f", {N} geodesic steps, {args.scene} scene"
+                             + (", test-ray overlay" if test_ray is not None else "") + ", percent_black "
                              + ("off" if args.percent_black < 0 else str(args.percent_black))
                              + (", flyby camera (a new camera every frame)" if args.camera == "flyby" else "")),
                 "width": W,
@@ -709,7 +720,7 @@ def main():
         rp["pricer"].close()
 
 
-def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_arg, no_cull, render, first,
+def single_frames(new_renderer, ctxs, cams, params, W, H, dev, split_arg, render, first,
                   restore=(0, 16, 1), frames=20, alone_reps=15, inflight=4):
     """Single-frame launches (sr_render_blocks of the whole frame): `alone` =
     one frame at a time, each waited for (median of alone_reps; HIP events on
@@ -726,11 +737,7 @@ def single_frames(pkg, ctxs, scene, skybox, arr, cams, params, W, H, dev, split_
     pool = [(c[0], c[1], c[3]) for c in ctxs[:inflight]]
     extra = []
     while len(pool) < inflight:
-        rk = pkg.Renderer(dev.index)
-        rk.set_scene(scene)
-        rk.set_background(skybox)
-        rk.set_texture_array(arr)
-        rk.set_culling(not no_cull)
+        rk = new_renderer()
         extra.append(rk)
         pool.append((rk, torch.zeros((1,) + tuple(ctxs[0][1].shape[1:]), dtype=torch.uint8, device=dev),
                      torch.cuda.Stream(dev)))
@@ -830,12 +837,18 @@ def frame_parity(args, W, H, N, quality, use_assets, frame, index):
     if not (args.camera == "static" and use_assets and args.mode == "curved" and args.percent_black < 0):
         out["reason"] = "no oracle fixture for these inputs"
         return out
+    variant = "stress" if args.scene == "stress" else ("testray" if args.test_ray == "on" else "default")
+    if args.scene == "stress" and args.test_ray == "on":
+        out["reason"] = "no oracle fixture for the stress scene with the test ray"
+        return out
     if not FRAME_HASHES.exists():
         out["reason"] = "tests/golden/frame_hashes.npz missing"
         return out
     with np.load(FRAME_HASHES) as z:
-        for cfg in ("c2", "c3", "c4", "c5"):
+        for cfg in sorted({k.split("/")[0] for k in z.files}):
             if f"{cfg}/config" not in z.files or tuple(int(v) for v in z[f"{cfg}/config"]) != (W, H, N):
+                continue
+            if (bytes(z[f"{cfg}/variant"]).decode() if f"{cfg}/variant" in z.files else "default") != variant:
                 continue
             if bytes(z[f"{cfg}/skybox"]).decode() != quality:
                 continue

@@ -2477,6 +2477,18 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #ifndef SR_NC_SMALL
 #define SR_NC_SMALL 1
 #endif
+#ifndef SR_GENERAL_WAVES_PER_EU
+#define SR_GENERAL_WAVES_PER_EU 5
+#endif
+
+// Waves per SIMD the integrate kernel is built for: SR_MIN_WAVES_PER_EU (6:
+// 80 VGPRs) for the frame kernels of scenes that fit the small
+// instantiation; 5 (96 VGPRs) for the general one (8 slots, 3 cylinders),
+// whose event path then keeps every value in registers (at 6 it spilled 9 in
+// the reseed path), its 6.5 KiB of LDS per wave allowing 24 waves per CU
+constexpr int sr_integrate_waves(int nb, int nc) {
+    return (nb > SR_NB_SMALL || nc > SR_NC_SMALL) ? SR_GENERAL_WAVES_PER_EU : SR_MIN_WAVES_PER_EU;
+}
 
 // Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
 // tile << 8 | SR_SPLIT | sub for workgroup `sub` of a split tile; -1 for an
@@ -2514,7 +2526,7 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // has six, and phase 1 of an event runs over every slot of the capacity).
 // NC: budgeted cylinders it handles (SR_NC_SMALL with SR_NB_SMALL).
 template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS>
-__global__ __launch_bounds__(SR_WG, SR_MIN_WAVES_PER_EU) void sr_integrate_kernel(
+__global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
     size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {

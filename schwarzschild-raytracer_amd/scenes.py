@@ -234,6 +234,53 @@ def scene_random(seed: int, n_objects: int = 21, translucent: bool = True, plane
     return s
 
 
+# The bench's max-capacity scene (bench.py --scene stress; BASELINE.md / the
+# verdict's "what the default scene hides"): every capacity of the uniform
+# block filled (frag:63-182): 3 of each primitive (21 objects, more than the
+# kernel's SR_MAX_BUDGET budget slots, so 13 are tested per chord), 10
+# materials, 4 lights. Fixed seed: tests/golden/frame_hashes.npz holds its
+# oracle frame (config "c2s").
+STRESS_SEED = 2024
+
+
+def scene_stress() -> abi.Scene:
+    s = scene_random(STRESS_SEED, n_objects=21, translucent=True, planes=True)
+    s.num_lights = abi.MAX_LIGHTS
+    rng = np.random.default_rng(STRESS_SEED + 1)
+    for i in range(abi.MAX_LIGHTS):
+        L = s.lights[i]
+        for k in range(3):
+            L.transform.pos[k] = float(np.float32(rng.uniform(-15, 15)))
+            L.color[k] = float(np.float32(rng.uniform(0.5, 1.0)))
+        L.intensity = float(np.float32(rng.uniform(2, 10)))
+        L.attenuation_constant, L.attenuation_linear, L.attenuation_quadratic = 1.0, 0.09, 0.032
+    return s
+
+
+# The press-R overlay of the bench (bench.py --test-ray on, src/main.cpp:375-391,
+# frag:760-803): the test ray traced from the app's camera position along
+# (3, -2, -15) (an escaping orbit; SURVEY App. B's second ray), its first
+# SR_MAX_POINTS = 1000 points as the curved polyline (1000 cylinders tested
+# against every chord) and the flat ray along the same direction.
+TEST_RAY_FROM = ((0.0, 2.0, 15.0), (3.0, -2.0, -15.0))
+TEST_RAY_STEPS = 2700  # 1000+ points of the press-R polyline
+
+
+def test_ray_overlay() -> abi.TestRay:
+    cam0 = camera_look(*TEST_RAY_FROM)
+    fwd = list(cam0.transform.axes[6:9])
+    pts = abi.test_ray_points(list(cam0.transform.pos), fwd, TEST_RAY_STEPS, 2)[:abi.MAX_POINTS]
+    tr = abi.default_test_ray()
+    tr.visible = 1
+    tr.num_curved_points = len(pts)
+    for i, p in enumerate(pts):
+        tr.curved_points[i][0], tr.curved_points[i][1], tr.curved_points[i][2] = p
+    for k in range(3):
+        tr.flat_origin[k] = cam0.transform.pos[k] + fwd[k]
+        tr.flat_dir[k] = fwd[k]
+    return tr
+
+
 def _axes_from(up, ref=(1.0, 0.0, 0.0)) -> list[float]:
     """Column-major orthonormal axes with axes[1] = normalize(up) (the plane
     normal / cylinder axis) and axes[0] in the plane of ref, float32."""

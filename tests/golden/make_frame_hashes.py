@@ -47,7 +47,13 @@ CONFIGS = {
     "c3": (1920, 1080, 2000, "2k"),
     "c4": (3840, 2160, 4000, "2k"),
     "c5": (7680, 4320, 8000, "8k"),
+    # config 2's size with what the default scene hides (bench.py --scene
+    # stress / --test-ray on): the max-capacity scene, and the default scene
+    # with the press-R overlay's 1000-point polyline
+    "c2s": (640, 360, 1000, "2k"),
+    "c2t": (640, 360, 1000, "2k"),
 }
+VARIANTS = {"c2s": "stress", "c2t": "testray"}  # the others: "default"
 CHUNK = 16
 
 
@@ -69,11 +75,14 @@ def frame_digest(row_sha: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(row_sha, dtype=np.uint8).tobytes()).hexdigest()
 
 
-def inputs(pkg, skybox: str):
+def inputs(pkg, skybox: str, variant: str = "default"):
+    """scene, camera, skybox, texture array and test ray (None: hidden) of a config"""
     A, sc, abi = pkg.assets, pkg.scenes, pkg.abi
     bg = A.skybox(skybox)
     arr, _, _ = A.texture_array()
-    return sc.scene_default(textured=True), abi.default_camera(), bg, arr
+    scene = sc.scene_stress() if variant == "stress" else sc.scene_default(textured=True)
+    test_ray = sc.test_ray_overlay() if variant == "testray" else None
+    return scene, abi.default_camera(), bg, arr, test_ray
 
 
 def ring_rows(H: int) -> list[int]:
@@ -93,7 +102,7 @@ def run(cfg: str, rows: list[int], threads: int) -> None:
     pkg = srpkg.load_package()
     oracle = srpkg.load_oracle()
     W, H, N, sky = CONFIGS[cfg]
-    scene, cam, bg, arr = inputs(pkg, sky)
+    scene, cam, bg, arr, test_ray = inputs(pkg, sky, VARIANTS.get(cfg, "default"))
     tex = oracle.TextureSet(bg, arr)
     params = pkg.abi.default_params(max_steps=N, percent_black=-1.0)
     WORK.mkdir(exist_ok=True)
@@ -114,7 +123,7 @@ def run(cfg: str, rows: list[int], threads: int) -> None:
                 if int(z["y1"]) >= y1:
                     done_rows += y1 - y0
                     continue
-        rgba8, _, steps = oracle.render(scene, cam, params, W, H, tex, None, y0, y1, threads)
+        rgba8, _, steps = oracle.render(scene, cam, params, W, H, tex, test_ray, y0, y1, threads)
         hr, hs = row_hashes(rgba8, steps)
         tmp = p.with_suffix(".tmp.npz")
         np.savez(tmp, y0=y0, y1=y1, rgba_sha=hr, steps_sha=hs, steps_sum=steps.astype(np.int64).sum(axis=1))
@@ -155,6 +164,7 @@ def merge() -> None:
         store[f"{cfg}/steps_sum"] = ss[rows]
         store[f"{cfg}/config"] = np.array([W, H, N], dtype=np.int32)
         store[f"{cfg}/skybox"] = np.frombuffer(sky.encode(), dtype=np.uint8)
+        store[f"{cfg}/variant"] = np.frombuffer(VARIANTS.get(cfg, "default").encode(), dtype=np.uint8)
         if len(rows) == H:
             store[f"{cfg}/frame_sha"] = np.frombuffer(bytes.fromhex(frame_digest(hr)), dtype=np.uint8)
         print(f"{cfg}: {len(rows)}/{H} rows, mean steps {ss[rows].sum() / (len(rows) * W):.2f}"

@@ -97,8 +97,9 @@ def frame_digest(rgba8):
 
 
 def test_fixture_covers_the_configs(fh):
-    """configs 2-5 in full (every row), each with its frame hash"""
-    for cfg, H in (("c2", 360), ("c3", 1080), ("c4", 2160), ("c5", 4320)):
+    """configs 2-5 and config 2's stress / test-ray variants in full (every
+    row), each with its frame hash"""
+    for cfg, H in (("c2", 360), ("c3", 1080), ("c4", 2160), ("c5", 4320), ("c2s", 360), ("c2t", 360)):
         assert len(fh[f"{cfg}/rows"]) == H, cfg
         assert f"{cfg}/frame_sha" in fh, cfg
 
@@ -258,4 +259,40 @@ def test_frame_gather_device_reassembly(pkg, fh, assets):
     assert tuple(frames.shape) == (3, H, W, 4)
     for f in range(3):
         compare(pkg, fh, "c3", frames[f].cpu().numpy(), None, f"FrameGather frame {f}")
+    r.close()
+
+
+@pytest.mark.parametrize("cfg,variant", [("c2s", "stress"), ("c2t", "testray")])
+def test_variant_frames_exact(pkg, fh, assets, cfg, variant):
+    """What the default scene hides, at config 2's size (bench.py --scene
+    stress / --test-ray on): the max-capacity scene (21 objects, 13 of them
+    tested per chord beside the 8 budget slots; 10 materials, 4 lights) and
+    the default scene with the press-R overlay's 1000-point polyline (1000
+    cylinders against every chord). The debug render (steps) and two batched
+    launches, every row against the oracle's hashes."""
+    import torch
+
+    W, H, N = (int(v) for v in fh[f"{cfg}/config"])
+    assert bytes(fh[f"{cfg}/variant"]).decode() == variant
+    abi, sc = pkg.abi, pkg.scenes
+    r = pkg.Renderer(0)
+    r.set_scene(sc.scene_stress() if variant == "stress" else sc.scene_default(textured=True))
+    r.set_background(assets["2k"])
+    r.set_texture_array(assets["arr"])
+    r.set_test_ray(sc.test_ray_overlay() if variant == "testray" else abi.default_test_ray())
+    params = abi.default_params(max_steps=N, percent_black=-1.0)
+    cam = abi.default_camera()
+    _, b, s = r.render_debug(cam, params, W, H)
+    torch.cuda.synchronize()
+    b, s = b.cpu().numpy(), s.cpu().numpy()
+    rows = fh[f"{cfg}/rows"]
+    assert not (sha_rows(b[rows]) != fh[f"{cfg}/rgba_sha"]).any(), f"{cfg}: RGBA8 rows differ"
+    assert not (sha_rows(s[rows].astype("<i4")) != fh[f"{cfg}/steps_sha"]).any(), f"{cfg}: step rows differ"
+    B = 4
+    for _ in range(2):
+        out, n = r.render_blocks_batch([cam] * B, params, W, H, BLOCK_ROWS, 0, 1)
+    torch.cuda.synchronize()
+    frames = out.cpu().numpy()
+    for f in range(B):
+        assert frame_digest(frames[f, :H]) == bytes(fh[f"{cfg}/frame_sha"]).hex(), f"{cfg}: batched frame {f}"
     r.close()

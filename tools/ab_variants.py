@@ -28,7 +28,9 @@ def main():
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--camera", default="default")
-    ap.add_argument("--scene", choices=["tex", "untex", "bh"], default="tex")
+    ap.add_argument("--scene", choices=["tex", "untex", "bh", "stress", "general"], default="tex",
+                    help="stress: scenes.scene_stress (21 objects); general: an 8-object random scene (every object "
+                         "in a budget slot, the general 8-slot / 3-cylinder instantiation)")
     ap.add_argument("--throughput", action="store_true",
                     help="bench.py's pipeline instead of single frames: --frames frames in launches of --batch "
                          "(sr_render_blocks_batch), --inflight launches in flight on their own contexts and streams")
@@ -42,7 +44,14 @@ def main():
 
     pkg = srpkg.load_package()
     abi, sc = pkg.abi, pkg.scenes
-    scene = sc.scene_black_hole_only() if args.scene == "bh" else sc.scene_default(textured=args.scene == "tex")
+    if args.scene == "bh":
+        scene = sc.scene_black_hole_only()
+    elif args.scene == "stress":
+        scene = sc.scene_stress()
+    elif args.scene == "general":
+        scene = sc.scene_random(7, n_objects=8, translucent=False, planes=False)
+    else:
+        scene = sc.scene_default(textured=args.scene == "tex")
     cam = abi.default_camera() if args.camera == "default" else sc.random_camera(int(args.camera))
     params = abi.default_params(max_steps=args.max_steps, percent_black=-1.0)
     bg = np.ascontiguousarray(sc.skybox(2048, 1024))
