@@ -161,14 +161,17 @@ def parse():
                          "of pixels of this rank's share per launch, at most half of --steps)")
     ap.add_argument("--split", default="0",
                     help="split tiles MAX_TILES[:LANES[:MIN_STEPS]] (sr_set_split; 0: off)")
-    ap.add_argument("--balance", choices=["cost", "cyclic"], default="cost",
+    ap.add_argument("--balance", choices=["auto", "cost", "cyclic"], default="auto",
                     help="N > 1: cost: each rank renders an equal number of 8-row blocks of about equal cost "
                          "(dist.balanced_blocks over the frame's step map, sr_render_block_list); cyclic: block b "
-                         "on rank b %% N")
+                         "on rank b %% N; auto: cost for the static camera (every frame is the priced one), cyclic "
+                         "for the flyby (block costs drift between frames by more than priced lists gain, "
+                         "dist.REPRICE_MARGIN)")
     ap.add_argument("--reprice", type=int, default=-1,
                     help="N > 1, --balance cost: re-price the block lists every this many launches from a "
-                         "quarter-resolution cost map of the launch's camera (rank 0, broadcast); -1: every "
-                         "launches-in-flight launches with --camera flyby, else never; 0: never")
+                         "quarter-resolution cost map of the launch's camera (rank 0, broadcast; the priced "
+                         "lists only when they beat cyclic rows by dist.REPRICE_MARGIN, else cyclic rows); -1: "
+                         "every launches-in-flight launches with --camera flyby, else never; 0: never")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl: RCCL gather of device tiles over xGMI (one GPU per rank); gloo: tiles staged "
                          "through host memory (ranks may share a GPU)")
@@ -391,7 +394,7 @@ def main():
 
     lists = [None]  # balanced_blocks lists (N > 1, --balance cost), set below from the step map
     sched = [None]  # dist.ListSchedule: the lists each context's launches render (re-pricing changes them)
-    rp = {"every": 0, "pricer": None, "stream": None}  # flyby re-pricing (set below)
+    rp = {"every": 0, "pricer": None, "stream": None, "choices": []}  # flyby re-pricing (set below)
 
     def render(rk, first, n, out, s_k, lst=None):
         """frames first .. first + n - 1 of this rank's share into out[:n]"""
@@ -417,8 +420,10 @@ def main():
             wc = rp["pricer"].wave_costs(cam, params, wl, hl, stream=rp["stream"])
             rp["stream"].synchronize()
             # a quarter-resolution 8-row block spans four full-resolution ones
-            cl = D.block_costs(wc.cpu())
-            obj = [D.balanced_blocks(np.repeat(cl, 4)[:D.nblocks(H, BLOCK_ROWS)], world)]
+            cl = np.repeat(D.block_costs(wc.cpu()), 4)[:D.nblocks(H, BLOCK_ROWS)]
+            lst, rp["last_choice"] = D.choose_lists(D.balanced_blocks(cl, world), cl, world, H, BLOCK_ROWS)
+            rp["choices"].append(rp["last_choice"])
+            obj = [lst]
         dist.broadcast_object_list(obj, src=0, device=None if gloo else dev)
         return obj[0]
 
@@ -472,7 +477,8 @@ def main():
     _, _, steps_full = r.render_debug(cams[0], params, W, H)
     torch.cuda.synchronize(dev)
     balance = None
-    if distributed and args.balance == "cost":
+    balance_used = args.balance if args.balance != "auto" else ("cost" if args.camera == "static" else "cyclic")
+    if distributed and balance_used == "cost":
         # rank 0 prices the blocks from the first frame's per-wave steps and
         # budget events and sends every rank the same lists (a rank whose own
         # cost map differed would otherwise render rows rank 0 does not expect)
@@ -586,17 +592,20 @@ def main():
     if balance is not None and rp["every"]:
         balance["reprice_every_launches"] = rp["every"]
         balance["repriced"] = sched[0].count
-        if rank == 0:  # how even the frame-0 lists and the lists in use are on the last timed camera
-            last_cam = cams[warm + args.steps - 1]
-            cost_last = D.block_costs(r.wave_costs(last_cam, params, W, H, stream=stream).cpu())
-
-            def mom(lst):
-                loads = [sum(cost_last[b] for b in l if b >= 0) for l in lst]
-                return round(max(loads) / (sum(loads) / world), 4)
-
-            balance["last_camera_max_over_mean"] = {"frame0_lists": mom(lists[0]),
-                                                    "lists_in_use": mom(sched[0].ctx[(len(range(warm, warm + args.steps, B)) - 1) % F]),
-                                                    "cyclic": mom([D.blocks_of(k, world, H, BLOCK_ROWS) for k in range(world)])}
+        if rank == 0:
+            balance["reprice_choices"] = rp["choices"]
+    last_camera = None
+    if distributed and args.camera == "flyby" and rank == 0:
+        # how even the lists in use (and the frame-0 lists, cyclic rows) are on
+        # the last timed camera, by its full-resolution cost map (untimed)
+        cost_last = D.block_costs(r.wave_costs(cams[warm + args.steps - 1], params, W, H, stream=stream).cpu())
+        cyclic_lists = [D.blocks_of(k, world, H, BLOCK_ROWS) for k in range(world)]
+        in_use = (sched[0].ctx[(len(range(warm, warm + args.steps, B)) - 1) % F] if sched[0] is not None
+                  else lists[0] if lists[0] is not None else cyclic_lists)
+        last_camera = {"lists_in_use": round(D.max_over_mean(in_use, cost_last), 4),
+                       "cyclic": round(D.max_over_mean(cyclic_lists, cost_last), 4)}
+        if lists[0] is not None:
+            last_camera["frame0_lists"] = round(D.max_over_mean(lists[0], cost_last), 4)
     ranks = None
     if distributed:  # max over ranks (RCCL reduces device tensors, gloo host ones)
         t = torch.tensor([elapsed, latency_ms], dtype=torch.float64, device=None if gloo else dev)
@@ -691,6 +700,8 @@ def main():
                             "the first frame), " if balance else f"block-cyclic {BLOCK_ROWS}-row bands over {world} rank(s), ")
                            + ("RCCL gather to rank 0" if not gloo else "gloo gather of host-staged tiles to rank 0")),
                 "balance": balance,
+                "balance_policy": {"requested": args.balance, "used": balance_used if distributed else None},
+                "last_camera_max_over_mean": last_camera,
                 "dist_backend": args.dist_backend if distributed else None,
                 "launches_in_flight": F,
                 "frames_per_launch": B,

@@ -2318,6 +2318,22 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
                     const int nl = __popcll(__ballot(event));
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
+#ifdef SR_STATS_TRIG  // measurement only (tools/stats_frame.py --trig): who spends which slot
+                    {
+                        // lanes whose own budget of slot j ran out (44 + j: orbiting the
+                        // photon sphere, 51 + j: the others) and events that re-anchor
+                        // slot j by the look-ahead alone (58 + j)
+                        const bool ring = r.u > 0.5f && r.u < 0.95f && fabsf(r.du) < 0.15f;
+                        const float Tt = bs.T();
+                        for (int j = 0; j < 7; j++) {
+                            const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
+                            const bool own = !(Tt < ej);
+                            SR_STAT(44 + j, __popcll(__ballot(own && ring)));
+                            SR_STAT(51 + j, __popcll(__ballot(own && !ring)));
+                            if (j < 6 && __ballot(!(Tt + ahead < ej)) && !__ballot(own)) SR_STAT(58 + j, 1);
+                        }
+                    }
+#else
                     if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
                     SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
                     SR_STAT(46, __popcll(__ballot(bhx)));
@@ -2340,6 +2356,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                         }
                     }
                     SR_STAT(54, any_cm);
+#endif
                 }
 #endif
                 // sr_wave_costs: the wave's event count (one lane, its own LDS word)

@@ -262,6 +262,34 @@ def assemble(stacked, world: int, height: int, block_rows: int):
     return v.reshape((per * world * block_rows,) + rest)[:height]
 
 
+def max_over_mean(lists, costs) -> float:
+    """The most loaded rank's cost over the mean (pads, -1, cost nothing)."""
+    loads = [sum(float(costs[b]) for b in lst if b >= 0) for lst in lists]
+    mean = sum(loads) / max(1, len(loads))
+    return max(loads) / mean if mean > 0 else 1.0
+
+
+# Block costs change from frame to frame of a moving camera by more than a
+# priced list gains over block-cyclic rows: over the bench's 8-rank flyby,
+# lists priced from the full-resolution map of one re-price camera scored
+# 1.018-1.031 max/mean on the cameras they were then used for, cyclic rows
+# 1.015-1.018 (profiles/r05/s2_reprice_*.jsonl, tools/reprice_eval.py).
+REPRICE_MARGIN = 0.02
+
+
+def choose_lists(priced, costs, world: int, height: int, block_rows: int, margin: float = REPRICE_MARGIN):
+    """Lists for the frames after a re-pricing: the newly priced lists only
+    when, under the map they were priced from, they beat block-cyclic rows by
+    more than `margin` (the map's own drift to the next frames); otherwise the
+    cyclic rows. Returns (lists, "priced" | "cyclic")."""
+    cyclic = [blocks_of(k, world, height, block_rows) for k in range(world)]
+    per = len(priced[0])
+    cyc = [c + [-1] * (per - len(c)) for c in cyclic]  # the same equal-length form
+    if max_over_mean(priced, costs) * (1.0 + margin) < max_over_mean(cyc, costs):
+        return priced, "priced"
+    return cyc, "cyclic"
+
+
 class ListSchedule:
     """The rank lists each launch renders when a moving camera re-prices them
     (bench.py --reprice). Launch j runs on context j % contexts; a launch whose

@@ -41,7 +41,7 @@ def run(cmd, out):
     return json.loads(line)
 
 
-@pytest.mark.parametrize("world,balance", [(2, "cost"), (3, "cost"), (2, "cyclic"), (8, "cost")])
+@pytest.mark.parametrize("world,balance", [(2, "cost"), (3, "cost"), (2, "cyclic"), (8, "cost"), (8, "auto")])
 def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
     try:
         import torch
@@ -55,16 +55,21 @@ def test_multi_rank_bench_frames_equal_single_rank(tmp_path, world, balance):
     bal = multi["config"]["balance"]
     if balance == "cost":
         assert bal["max_over_mean"] <= bal["cyclic_max_over_mean"] + 1e-9, bal
-    else:
+    else:  # auto with the flyby: cyclic rows (dist.REPRICE_MARGIN)
         assert bal is None
+    assert multi["config"]["balance_policy"]["used"] == ("cost" if balance == "cost" else "cyclic")
     assert multi["config"]["dist_backend"] == "gloo" and multi["config"]["launches_in_flight"] == 3
     ranks = multi["config"]["ranks"]  # the N-rank line documents every rank
     assert [r["rank"] for r in ranks] == list(range(world)) and all(r["world_size"] == world for r in ranks)
     assert all(r["share_ms_per_frame"] > 0 and r["gather_ms_per_frame"] >= 0 for r in ranks)
+    lc = multi["config"]["last_camera_max_over_mean"]
+    assert lc["lists_in_use"] >= 1.0 and lc["cyclic"] >= 1.0
     if balance == "cost":  # the flyby re-prices the lists while frames are in flight
         assert bal["lists_from"] == "rank 0 (broadcast)" and bal["repriced"] >= 1, bal
-        lc = bal["last_camera_max_over_mean"]
-        assert lc["lists_in_use"] >= 1.0 and lc["frame0_lists"] >= 1.0
+        assert set(bal["reprice_choices"]) <= {"priced", "cyclic"} and len(bal["reprice_choices"]) == bal["repriced"]
+        assert lc["frame0_lists"] >= 1.0
+    else:
+        assert lc["lists_in_use"] == lc["cyclic"]
     one = sorted((tmp_path / "one").glob("frame_*.npy"))
     many = sorted((tmp_path / "multi").glob("frame_*.npy"))
     assert len(one) == len(many) == 12

@@ -110,3 +110,26 @@ def test_list_schedule_every_context_adopts_repriced_lists(pkg):
     never = D.ListSchedule("L0", 3, 0, 8)
     assert not any(never.due(f) for f in range(0, 400, 8))
     assert never.adopt(5) == ("L0", False)
+
+
+def test_reprice_falls_back_to_cyclic_rows(pkg):
+    """A re-pricing keeps the priced lists only when they beat block-cyclic
+    rows by more than the inter-frame drift margin (dist.REPRICE_MARGIN) under
+    the map they were priced from; otherwise every rank gets its cyclic rows
+    (padded to the lists' length). bench.py --camera flyby --balance auto uses
+    cyclic rows outright."""
+    D = pkg.dist
+    H, rows, world = 1080, 8, 8
+    nb = D.nblocks(H, rows)
+    rng = np.random.default_rng(5)
+    flat = rng.uniform(1.0, 1.001, nb)  # priced lists cannot beat cyclic by 2 % here
+    lists, how = D.choose_lists(D.balanced_blocks(flat, world), flat, world, H, rows)
+    assert how == "cyclic"
+    assert [[b for b in l if b >= 0] for l in lists] == [D.blocks_of(k, world, H, rows) for k in range(world)]
+    assert len({len(l) for l in lists}) == 1  # equal-length lists (pads)
+    skew = np.where(np.arange(nb) % world == 0, 50.0, 1.0)  # cyclic rows put every heavy block on rank 0
+    priced = D.balanced_blocks(skew, world)
+    lists, how = D.choose_lists(priced, skew, world, H, rows)
+    assert how == "priced" and lists == priced
+    assert D.max_over_mean(priced, skew) < D.max_over_mean(
+        [D.blocks_of(k, world, H, rows) for k in range(world)], skew) / (1 + D.REPRICE_MARGIN)

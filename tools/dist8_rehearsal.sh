@@ -13,12 +13,19 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 
   --master-port 29517 bench.py --gpus 8 --steps 20 --warmup 3 --dist-backend gloo > "$OUT/bench8.log" 2>&1 \
   || { echo "bench8 rc=$?"; tail -n 30 "$OUT/bench8.log"; exit 1; }
 grep '^{' "$OUT/bench8.log" > "$OUT/bench8.json"; cat "$OUT/bench8.json"
-# the flyby at N = 8: lists re-priced every 3 launches (default) and frame-0 lists kept
-for rp in -1 0; do
+# the flyby at N = 8: the default (auto: cyclic rows for a moving camera),
+# cost lists re-priced every 3 launches, and the frame-0 cost lists kept
+for v in "auto -1" "cost -1" "cost 0"; do
+  set -- $v
   timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-    --master-port 29518 bench.py --gpus 8 --steps 40 --warmup 3 --dist-backend gloo --camera flyby --reprice $rp \
-    --cpu-baseline off > "$OUT/bench8_flyby_rp$rp.log" 2>&1 || { echo "bench8 flyby rc=$?"; tail -n 30 "$OUT/bench8_flyby_rp$rp.log"; exit 1; }
-  grep '^{' "$OUT/bench8_flyby_rp$rp.log" > "$OUT/bench8_flyby_rp$rp.json"
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], json.dumps(d['config']['balance']))" "$OUT/bench8_flyby_rp$rp.json"
+    --master-port 29518 bench.py --gpus 8 --steps 40 --warmup 3 --dist-backend gloo --camera flyby --balance $1 \
+    --reprice $2 --cpu-baseline off > "$OUT/bench8_flyby_$1_rp$2.log" 2>&1 || { echo "bench8 flyby rc=$?"; tail -n 30 "$OUT/bench8_flyby_$1_rp$2.log"; exit 1; }
+  grep '^{' "$OUT/bench8_flyby_$1_rp$2.log" > "$OUT/bench8_flyby_$1_rp$2.json"
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print(sys.argv[1], d['value'], c['balance_policy'], c['last_camera_max_over_mean'], (c['balance'] or {}).get('reprice_choices'))" "$OUT/bench8_flyby_$1_rp$2.json"
 done
+# the driver's own shape: bench.py --gpus 8 without a launcher (it spawns its ranks)
+timeout -k 10 400 python bench.py --gpus 8 --steps 20 --warmup 3 --dist-backend gloo --cpu-baseline off > "$OUT/bench8_spawn.log" 2>&1 \
+  || { echo "bench8 spawn rc=$?"; tail -n 30 "$OUT/bench8_spawn.log"; exit 1; }
+grep '^{' "$OUT/bench8_spawn.log" > "$OUT/bench8_spawn.json"
+python -c "import json,sys; d=json.load(open(sys.argv[1])); print('spawned', d['n_gpus'], d['config']['world_size'], d['parity'])" "$OUT/bench8_spawn.json"
 echo "session done"

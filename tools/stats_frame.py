@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
     ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080], help="render only rows [a, b) (waves alone on the chip)")
+    ap.add_argument("--trig", action="store_true", help="an SR_STATS_TRIG build (counters 44..63)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -78,6 +79,12 @@ def main():
              "interval1_triggered", "interval1_reseeded", "interval1_budget_below_0.05", "interval1_cm_events",
              "cm_events"])}
         out["interval1_small_budget_lanes_by_slot"] = [int(hi[23 + j]) for j in range(9)]
+        if args.trig:  # an SR_STATS_TRIG build: counters 44..63 hold the lanes that spent each slot
+            for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
+                out.pop(k, None)
+            out["own_spent_lanes_ring"] = [int(hi[12 + j]) for j in range(7)]
+            out["own_spent_lanes_other"] = [int(hi[19 + j]) for j in range(7)]
+            out["lookahead_only_events"] = [int(hi[26 + j]) for j in range(6)]
     # wave timeline of the integrate kernel (lane 0 of each wave that had pixels)
     import numpy as np
 
