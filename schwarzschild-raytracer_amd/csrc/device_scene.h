@@ -58,8 +58,13 @@
 #ifndef SR_BUDGET_TMAX
 #define SR_BUDGET_TMAX 32.0f
 #endif
-// Objects held in the per-lane budget registers (index 0 is the black hole).
-#define SR_MAX_BUDGET 8
+// Objects held in per-lane budget slots (slot 0 is the black hole): every
+// object of a full scene (SR_MAX_OBJECTS). The integrate kernel is
+// instantiated for 6 (the default scene), 8 and all 21 slots
+// (geodesic.hip sr_launch_geodesic).
+#ifndef SR_MAX_BUDGET
+#define SR_MAX_BUDGET SR_MAX_OBJECTS
+#endif
 
 typedef struct {
     int32_t type;
@@ -106,12 +111,26 @@ typedef struct {
 
 // One test-ray cylinder: pos[3] axes[9] height radius, padded to 16 floats.
 #define SR_SEG_FLOATS 16
+// Culling bounds of the curved test ray (geodesic.hip test_ray_hits_culled),
+// after the segments in the same buffer: blocks of SR_TR_BLOCK consecutive
+// segments, then groups of SR_TR_GROUP blocks. A bound is {centre[3], R,
+// cone axis[3], cos alpha, sin alpha, max |pos|_1, always (1: no culling), -}:
+// every segment's may_hit sphere (bc, br) lies within R of the centre, every
+// segment axis within alpha of the cone axis.
+#define SR_TR_BLOCK 8
+#define SR_TR_GROUP 8
+#define SR_TR_BLOCKS ((SR_MAX_POINTS - 1 + SR_TR_BLOCK - 1) / SR_TR_BLOCK)
+#define SR_TR_GROUPS ((SR_TR_BLOCKS + SR_TR_GROUP - 1) / SR_TR_GROUP)
+#define SR_TR_BOUND_FLOATS 12
+#define SR_SEGS_BUF_FLOATS ((SR_MAX_POINTS - 1) * SR_SEG_FLOATS + (SR_TR_BLOCKS + SR_TR_GROUPS) * SR_TR_BOUND_FLOATS)
 
 typedef struct {
     int32_t num_objects;
     int32_t num_lights;
     int32_t tr_visible;
     int32_t tr_num_segments;  // num_test_ray_curved_points - 1 (>= 0)
+    int32_t tr_num_blocks;    // culling blocks / groups of the segments (SR_TR_BLOCK, SR_TR_GROUP)
+    int32_t tr_num_groups;
     float tr_radius;
     float tr_extended_length;
     int32_t num_budget;       // objects of SR_KIND_BUDGET (<= SR_MAX_BUDGET)

@@ -94,6 +94,8 @@ struct Tex {
     const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
+// budget slots 0 .. 8 have their own counters in measurement builds
+#define SR_STATS_SLOTS 9
 #ifdef SR_STATS
 // Measurement builds only: wave-level event counters (tools/stats_frame.py).
 //   0 wave-steps  1 budget events  2..10 slot j reached (exact chord)
@@ -1124,7 +1126,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     const uint32_t xcl = SR_XPLANE ? bs.excl() : 0u;  // slots off this orbit's plane (budget_frame)
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
-        SR_STAT(14 + j, 1);
+        if (j <= 8) SR_STAT(14 + j, 1);
 #ifdef SR_PROF
         if (j < 8 && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[8 + j] += 1;
 #endif
@@ -1215,6 +1217,67 @@ __device__ __forceinline__ void test_ray_hits(const sr_dev_scene* __restrict__ s
     }
 }
 
+// Culled test-ray hits for one exact chord [o, o + seg d] of the step loop
+// (frag:760-803: the flat cylinder, then every curved segment). A segment is
+// skipped only when the chord stays beyond the reach may_hit would give a
+// budgeted cylinder of its pose (bounding sphere + mu S + the quadratic's
+// root-error margin SR_CYL_QMARGIN Sc^2 / (r |d_perp|^2)), the rule that culls
+// the scene's own cylinders; decided for a whole block or group of segments
+// at once (sr_api.cpp test_ray_bounds: every segment's sphere lies within R
+// of the bound's centre, its axis within alpha of the cone axis, so |d_perp|^2
+// >= 1 - cos^2(phi - alpha) for a chord at angle phi from the cone axis). The
+// survivors are the exhaustive loop's tests with the same keys, so the
+// winner is the same.
+__device__ __forceinline__ bool tr_bound_may_hit(const float* __restrict__ B, f3 o, f3 d, float seg, float S, float r) {
+    if (B[10] != 0.0f) return true;  // a segment without a proven bound
+    const f3 w = ld3(B) - o;
+    float t = dot(w, d);
+    t = t < 0.0f ? 0.0f : t;
+    t = t > seg ? seg : t;
+    const f3 q = w - d * t;
+    const float d2 = dot(q, q);
+    const float cphi = fabsf(dot(d, ld3(B + 4)));
+    const float cosa = B[7], sina = B[8];
+    // max over the block of |d . a1_k| <= cos(phi - alpha) for phi > alpha
+    const float sphi = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cphi * cphi));
+    const float maxc = cphi >= cosa ? 1.0f : fminf(1.0f, __builtin_fmaf(cphi, cosa, sphi * sina) * 1.00001f + 1.0e-6f);
+    const float dp = 1.0f - maxc * maxc;
+    if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
+    const float Sc = S + B[9];
+    const float R = (B[3] + SR_MU_PLANAR * S + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp)) * 1.001f;
+    return !(d2 > R * R);
+}
+__device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                                     Hit& best, f3 o, f3 d, float seg) {
+    if (!sc->tr_visible) return;
+    f3 p;
+    const float* t = sc->tr_flat;
+    const m3 A = ldm(t + 3);
+    consider(best, cyl_test(o, d, ld3(t), A, t[12], t[13], seg, p), p, o, SLOT_TR_FLAT, 0, KEY_TR_FLAT);
+    const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;  // as closest_hit_chord's may_hit
+    const float r = sc->tr_radius;
+    const float* blocks = segs + (SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
+    const float* groups = blocks + SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
+    const int ns = sc->tr_num_segments, nb = sc->tr_num_blocks, ng = sc->tr_num_groups;
+    for (int g = 0; g < ng; g++) {
+        const bool hg = tr_bound_may_hit(groups + g * SR_TR_BOUND_FLOATS, o, d, seg, S, r);
+        if (!__ballot(hg)) continue;
+        const int b1 = min(nb, (g + 1) * SR_TR_GROUP);
+        for (int b = g * SR_TR_GROUP; b < b1; b++) {
+            const bool hb = hg && tr_bound_may_hit(blocks + b * SR_TR_BOUND_FLOATS, o, d, seg, S, r);
+            if (!__ballot(hb)) continue;
+            const int s1 = min(ns, (b + 1) * SR_TR_BLOCK);
+            for (int s = b * SR_TR_BLOCK; s < s1; s++) {
+                if (!hb) continue;
+                const float* q = segs + s * SR_SEG_FLOATS;
+                const m3 B = ldm(q + 3);
+                consider(best, cyl_test(o, d, ld3(q), B, q[12], q[13], seg, p), p, o, SLOT_TR_CURVED, 0,
+                         KEY_TR_CURVED0 + s);
+            }
+        }
+    }
+}
+
 // intersect(), frag:755-814, exhaustively: the closest hit along
 // [o, o + max_lambda*d] (max_lambda < 0: unbounded).
 __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
@@ -1237,7 +1300,7 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                                  uint32_t reach, f3 o, f3 d, float seg) {
     Hit best = no_hit();
-    test_ray_hits(sc, segs, best, o, d, seg);
+    test_ray_hits_culled(sc, segs, best, o, d, seg);
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
@@ -1719,12 +1782,15 @@ struct Ray {
     f3 ro, rd, nv, tv;
     float u, du;
     int i, steps;
+#ifdef SR_DEBUG_PX  // debugging builds only: printf trace of one pixel (x, y, kernel)
+    int dbg;
+#endif
 #ifdef SR_PROF
     unsigned* prof;  // the wave's 8 section accumulators in LDS
 #endif
 #ifdef SR_STATS
     int ev, mat;  // budget events, exact chords (measurement builds)
-    int rc[SR_MAX_BUDGET + 1];
+    int rc[SR_STATS_SLOTS];
 #endif
 };
 
@@ -1819,7 +1885,7 @@ __device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const sr_dev_c
 #ifdef SR_STATS
     r.ev = 0;
     r.mat = 0;
-    for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] = 0;
+    for (int j = 0; j < SR_STATS_SLOTS; j++) r.rc[j] = 0;
 #endif
     const bool flat = fr.raytrace_type == SR_RAYTRACE_FLAT ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_WIDTH && uv.x > 2.0f * fr.curved_percentage + -1.0f) ||
@@ -1890,13 +1956,26 @@ __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 // non-subnormal q (the stage values here are never subnormal: DESIGN.md §4);
 // and 2 q is exact, so fma(2, q, a) is the rounding of a + 2 q, as the
 // reference's a + (2. * q).
+// SR_TABLE16: the step table's entry is one float4 {h, h / 6, cos phi, sin
+// phi} (16 bytes: half the scalar loads and SGPRs of the two-float4 entry
+// with 0.5 h), and a + q (0.5 h) is computed as fma(0.5, q h, a): q (0.5 h),
+// (0.5 q) h and 0.5 (q h) are all the rounding of the same product (scaling
+// by 0.5 is exact), and the fused add of the exact 0.5 (q h) rounds once, as
+// the reference's separate add does.
+#ifndef SR_TABLE16
+#define SR_TABLE16 0
+#endif
+#define SR_TBL_STRIDE (SR_TABLE16 ? 1 : 2)  // float4 per step of the step table
+__device__ __forceinline__ float half_step(float a, float q, float h, float hh) {
+    return SR_TABLE16 ? __builtin_fmaf(0.5f, q * h, a) : a + q * hh;
+}
 __device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, float h6, float& un, float& dun) {
     const float k1 = du;
     const float l1 = ddu(u);
-    const float k2 = du + l1 * hh;
-    const float l2 = ddu(u + k1 * hh);
-    const float k3 = du + l2 * hh;
-    const float l3 = ddu(u + k2 * hh);
+    const float k2 = half_step(du, l1, h, hh);
+    const float l2 = ddu(half_step(u, k1, h, hh));
+    const float k3 = half_step(du, l2, h, hh);
+    const float l3 = ddu(half_step(u, k2, h, hh));
     const float k4 = du + l3 * h;
     const float l4 = ddu(u + k3 * h);
     un = u + h6 * (__builtin_fmaf(2.0f, k3, __builtin_fmaf(2.0f, k2, k1)) + k4);
@@ -1977,7 +2056,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     // {cos phi, sin phi} after step j (step -1: the camera, phi = 0)
     auto phi_cs = [&](int j) -> f2 {
         if (j < 0) return F2(1.0f, 0.0f);
-        const float4 t = tbl[2 * j];
+        const float4 t = tbl[SR_TBL_STRIDE * j];
         return F2(t.z, t.w);
     };
     // materialise the chord of step i - 1 (its end point from r.u, its start
@@ -2070,7 +2149,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const bool any_cm = CULL && __ballot(bcm != 0u);
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
-        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + 2 * i);
+        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + SR_TBL_STRIDE * i);
         float4 e;
         float un, dun, rB;
         uint32_t par;
@@ -2091,9 +2170,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             constexpr int CMV = decltype(cm_tag)::value;
             constexpr bool CM = CMV != 0;
             par = 0;
-            float4 e1;
+            float4 e1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             e = ldc(tp);
-            e1 = ldc(tp + 1);
+            if (!SR_TABLE16) e1 = ldc(tp + 1);
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs<NC> cd = CM ? cyl_dirs(sc, bs) : CylDirs<NC>{};
             const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bm, bs.mh()), bcx, bcy)) : q0;
@@ -2135,7 +2214,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.u = un;
                 r.du = dun;
                 if (CMV == 1) rA = rB;
-                tp += 2;
+                tp += SR_TBL_STRIDE;
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
                 e1 = en1;
@@ -2149,19 +2228,20 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // they are issued (sunk to their first use, they would be waited
             // at once).
             for (;;) {
+                constexpr int S = SR_TBL_STRIDE;
                 float4 nx[2 * FU];
 #pragma unroll
-                for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
+                for (int k = 0; k < S * FU; k++) nx[k] = ldc(tp + S + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     if (compute(k)) {
 #pragma unroll
-                        for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = S * k; j < S * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
-                        leave = apply(nx[2 * k], nx[2 * k + 1]);
+                        leave = apply(nx[S * k], S == 2 ? nx[S * k + 1] : e1);
                     }
                 }
                 if (leave) break;
@@ -2176,13 +2256,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // the iterates are the same. Only outward lanes (u < 0.6 falling)
         // coast: u stays finite.
         auto coast = [&]() {
-            float4 e1;
+            constexpr int S = SR_TBL_STRIDE;
+            float4 e1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             e = ldc(tp);
-            e1 = ldc(tp + 1);
+            if (!SR_TABLE16) e1 = ldc(tp + 1);
             for (;;) {
                 float4 nx[2 * FU];
 #pragma unroll
-                for (int k = 0; k < 2 * FU; k++) nx[k] = ldc(tp + 2 + k);
+                for (int k = 0; k < S * FU; k++) nx[k] = ldc(tp + S + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
@@ -2191,16 +2272,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(0, 1);
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
-                    if (__ballot(un < ulo || un > uhi)) {
+                    if (__ballot(!(un >= ulo && un <= uhi))) {  // NaN leaves too
 #pragma unroll
-                        for (int j = 2 * k; j < 2 * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = S * k; j < S * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
                         r.u = un;
                         r.du = dun;
-                        tp += 2;
-                        e = nx[2 * k];
-                        e1 = nx[2 * k + 1];
+                        tp += S;
+                        e = nx[S * k];
+                        if (S == 2) e1 = nx[S * k + 1];
                         leave = ++i >= N;
                     }
                 }
@@ -2223,7 +2304,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             if (ie == ick) return upck;
             float u = uck, du = duck;
             for (int j = ick; j < ie - 1; j++) {  // steps ick .. ie - 2
-                const float4 t0 = tbl[2 * j], t1 = tbl[2 * j + 1];
+                const float4 t0 = tbl[SR_TBL_STRIDE * j];
+                const float4 t1 = SR_TABLE16 ? t0 : tbl[2 * j + 1];
                 float un2, dun2;
                 rk4_step(u, du, t0.x, t1.y, t0.y, un2, dun2);  // the fast loop's operands
                 u = un2;
@@ -2262,7 +2344,17 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const bool bhx = un > uhi || (un < SR_BH_ULO2 && uhi == SR_BH_U2);
         // a chord ending beyond 2 / u_f, which the orbital-plane exclusions do
         // not cover (budget_frame): an event that forces them (budget_event)
-        const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f);
+        // a ray through the singularity (u past 1e30: its chord points round
+        // to the origin, then inf / NaN): the exact chord is degenerate (zero
+        // length, NaN direction) and the exact tests decide what its NaN
+        // arithmetic hits, so every slot is tested (reach below)
+        const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
+        const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
+#ifdef SR_DEBUG_PX
+        if (r.dbg)
+            printf("[%d] slow i %d u %.9g un %.9g du %.9g vb %g bhx %d ev %d uhi %g E0 %g T %g m %g excl %x\n", r.dbg, i,
+                   r.u, un, r.du, vb, (int)bhx, (int)event, uhi, bs.E[0], bs.T(), bs.m(), bs.excl());
+#endif
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
@@ -2403,11 +2495,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
                                      fr.u_f);
+                if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
                 SR_PT(6);
 #ifdef SR_STATS
-                for (uint32_t c = reach; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
+                for (uint32_t c = reach & 0x1ffu; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
 #pragma unroll
-                for (int j = 0; j <= SR_MAX_BUDGET; j++) r.rc[j] += (reach >> j) & 1u;
+                for (int j = 0; j < SR_STATS_SLOTS; j++) r.rc[j] += (reach >> j) & 1u;
 #endif
                 if (!__ballot(reach != 0u || every)) break;
 #ifdef SR_STATS_FIRE
@@ -2425,6 +2518,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             float seg = len(delta);
             r.rd = delta / seg;
             hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
+#ifdef SR_DEBUG_PX
+            if (r.dbg)
+                printf("[%d] exact i %d reach %x hit slot %d dist %g |prev| %g |ro| %g\n", r.dbg, i, reach, hit.slot, hit.dist,
+                       len(prev), len(r.ro));
+#endif
             SR_PT(4);
             if (hit.slot != SLOT_NONE) {
                 const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
@@ -2497,6 +2595,12 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #ifndef SR_GENERAL_WAVES_PER_EU
 #define SR_GENERAL_WAVES_PER_EU 5
 #endif
+// the general instantiation: 8 slots, 3 cylinders (25 LDS rows); scenes with
+// more budget slots run the large one (every object budgeted: SR_MAX_BUDGET
+// slots, 38 rows, 9.5 KiB of LDS per wave: 16 waves per CU, 4 per SIMD)
+#define SR_NB_GENERAL 8
+#define SR_NC_GENERAL SR_MAX_CYLINDERS
+#define SR_LARGE_WAVES_PER_EU 4
 
 // Waves per SIMD the integrate kernel is built for: SR_MIN_WAVES_PER_EU (6:
 // 80 VGPRs) for the frame kernels of scenes that fit the small
@@ -2504,7 +2608,8 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 // whose event path then keeps every value in registers (at 6 it spilled 9 in
 // the reseed path), its 6.5 KiB of LDS per wave allowing 24 waves per CU
 constexpr int sr_integrate_waves(int nb, int nc) {
-    return (nb > SR_NB_SMALL || nc > SR_NC_SMALL) ? SR_GENERAL_WAVES_PER_EU : SR_MIN_WAVES_PER_EU;
+    return nb > SR_NB_GENERAL ? SR_LARGE_WAVES_PER_EU
+                              : (nb > SR_NB_SMALL || nc > SR_NC_SMALL) ? SR_GENERAL_WAVES_PER_EU : SR_MIN_WAVES_PER_EU;
 }
 
 // Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
@@ -2574,7 +2679,7 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
     const unsigned long long c_start = __builtin_amdgcn_s_memtime();  // shader clock: the in-kernel clock (rec[15])
     unsigned long long evmat = 0;
-    int rcv[SR_MAX_BUDGET + 1] = {};
+    int rcv[SR_STATS_SLOTS] = {};
 #endif
     Pix q;
     int steps = 0;
@@ -2595,6 +2700,10 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         Ray r;
         Hit hit;
         int st = init_pixel(fr, fr.cam[frame], q, r);
+#ifdef SR_DEBUG_PX
+        r.dbg = (q.px == SR_DEBUG_PX && q.py == SR_DEBUG_PY) ? 1 : 0;
+        if (r.dbg) printf("[1] init st %d u %.9g du %.9g\n", st, r.u, r.du);
+#endif
 #ifdef SR_LANE_MASK  // latency experiments only (tools/lane_mask.py): masked pixels run no ray
         if (sr_lane_mask && !sr_lane_mask[(size_t)q.py * fr.width + q.px]) st = ST_DONE;
 #endif
@@ -2603,6 +2712,9 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[23] += (unsigned)(clock64() - prof_t0);
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
+#ifdef SR_DEBUG_PX
+        if (r.dbg) printf("[1] end st %d steps %d logged %d i %d\n", st, r.steps, log.n, r.i);
+#endif
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
@@ -2622,7 +2734,7 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         steps = r.steps;
 #ifdef SR_STATS
         evmat = ((unsigned long long)r.ev << 32) | (unsigned)r.mat;
-        for (int j = 0; j <= SR_MAX_BUDGET; j++) rcv[j] = r.rc[j];
+        for (int j = 0; j < SR_STATS_SLOTS; j++) rcv[j] = r.rc[j];
 #endif
     }
 #ifdef SR_STATS
@@ -2634,8 +2746,8 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
             const unsigned long long o = __shfl_xor(em, off);
             em = o > em ? o : em;
         }
-        int rcm[SR_MAX_BUDGET + 1];
-        for (int j = 0; j <= SR_MAX_BUDGET; j++) {
+        int rcm[SR_STATS_SLOTS];
+        for (int j = 0; j < SR_STATS_SLOTS; j++) {
             rcm[j] = rcv[j];
             for (int off = 32; off > 0; off >>= 1) rcm[j] = max(rcm[j], __shfl_xor(rcm[j], off));
         }
@@ -2646,7 +2758,7 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
             rec[1] = __builtin_amdgcn_s_memrealtime();
             rec[2] = (unsigned long long)sm;
             rec[3] = em;
-            for (int j = 0; j <= SR_MAX_BUDGET; j++) rec[4 + j] = (unsigned long long)rcm[j];
+            for (int j = 0; j < SR_STATS_SLOTS; j++) rec[4 + j] = (unsigned long long)rcm[j];
             rec[13] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
             rec[14] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (wave, SIMD, CU, SE)
             rec[15] = __builtin_amdgcn_s_memtime() - c_start;     // shader-clock cycles of the wave
@@ -2851,6 +2963,10 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         r.du = ps.at(PS_DU, id);
         r.i = ps.geti(PS_I, id) + 1;
         r.steps = (int)((unsigned)__float_as_int(rec.x) >> 8);
+#ifdef SR_DEBUG_PX
+        r.dbg = (q.px == SR_DEBUG_PX && q.py == SR_DEBUG_PY) ? 2 : 0;
+        if (r.dbg) printf("[2] resume i %d steps %d u %.9g du %.9g\n", r.i, r.steps, r.u, r.du);
+#endif
         HitLog log{ps, 0};  // RECORD = false: nothing is logged
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();
@@ -2893,10 +3009,16 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (nblocks > (1u << 22)) return hipErrorInvalidValue;  // tile << 8 stays a positive int
     const unsigned slots = nblocks + ((64u >> (split ? fr->split_log2 : 6)) - 1u) * (unsigned)split;
     const bool cull = fr->cull != 0;
-    // the small instantiation (6 slots, 1 cylinder: 17 LDS rows) when the scene fits it
+    // the small instantiation (6 slots, 1 cylinder: 17 LDS rows) when the
+    // scene fits it, the general one (8 slots) or the large one (every object)
     const bool small = cull && fr->num_budget <= SR_NB_SMALL && fr->num_budget_cyl <= SR_NC_SMALL;
+    const bool general = fr->num_budget <= SR_NB_GENERAL;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
-    if (fr->wave_cost)
+    if (fr->wave_cost && general)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, true, SR_NB_GENERAL, SR_FAST_UNROLL, SR_NC_GENERAL>),
+                           dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
+                           sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (small && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
@@ -2906,12 +3028,16 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
         hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, SR_FAST_UNROLL, SR_NC_SMALL>),
                            dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (cull && general)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_GENERAL, SR_FAST_UNROLL, SR_NC_GENERAL>),
+                           dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
+                           tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (cull)
         hipLaunchKernelGGL(sr_integrate_kernel<true>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
                            tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
-    else
-        hipLaunchKernelGGL(sr_integrate_kernel<false>, dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc,
-                           tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else  // the reference's loop (no budgets: the smallest LDS layout)
+        hipLaunchKernelGGL((sr_integrate_kernel<false, false, 1, SR_FAST_UNROLL, 1>), dim3(slots * B * SR_WG_PER_TILE),
+                           dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
     hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
                        out, pitch, dbg_rgba, dbg_steps, list, count, diag);

@@ -304,6 +304,80 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
     }
 }
 
+// Culling bounds of the curved test ray's segments (device_scene.h
+// SR_TR_BLOCK / SR_TR_GROUP; geodesic.hip test_ray_hits_culled). Per segment
+// k the sphere may_hit would use for a budgeted cylinder of that pose (set_bound:
+// bc = pos + a1 h / 2, br = R + 1e-4 (1 + |bc|_1 + R), R = sqrt(r^2 + (h / 2)^2))
+// and its axis a1; a bound covers its segments' spheres (R_bound >= |bc_k - c|
+// + br_k) and axes (within alpha of the cone axis), with |pos|_1 at most pl1.
+// Segments whose frame is not orthonormal (or not finite), a zero radius,
+// make their block and group `always` (no culling).
+void test_ray_bounds(float* buf, int nseg, float r, int& nblocks, int& ngroups) {
+    struct Seg {
+        double bc[3], br, ax[3], pl1;
+        bool ok;
+    };
+    std::vector<Seg> sg((size_t)nseg);
+    for (int k = 0; k < nseg; k++) {
+        const float* g = buf + (size_t)k * SR_SEG_FLOATS;
+        Seg& q = sg[(size_t)k];
+        const V3 a0 = ld(g + 3), a1 = ld(g + 6), a2 = ld(g + 9);
+        const float h = g[12];
+        q.ok = orthonormal(a0, a1, a2) && h >= 0.f && r > 0.f && std::isfinite(h) && std::isfinite(r);
+        const V3 bc = add(ld(g), scl(a1, 0.5f * h));
+        const double R = std::sqrt((double)r * r + 0.25 * (double)h * h);
+        q.bc[0] = bc.x, q.bc[1] = bc.y, q.bc[2] = bc.z;
+        q.br = (R + 1e-4 * (1.0 + std::fabs(q.bc[0]) + std::fabs(q.bc[1]) + std::fabs(q.bc[2]) + R)) * (1.0 + 1e-6);
+        q.ax[0] = a1.x, q.ax[1] = a1.y, q.ax[2] = a1.z;
+        q.pl1 = std::fabs((double)g[0]) + std::fabs((double)g[1]) + std::fabs((double)g[2]);
+        q.ok = q.ok && std::isfinite(q.br) && std::isfinite(q.pl1);
+    }
+    // bound of segments [k0, k1) into out[SR_TR_BOUND_FLOATS]
+    auto bound = [&](int k0, int k1, float* out) {
+        double c[3] = {0, 0, 0}, ca[3] = {0, 0, 0};
+        bool ok = k1 > k0;
+        for (int k = k0; k < k1; k++) {
+            ok = ok && sg[(size_t)k].ok;
+            for (int i = 0; i < 3; i++) {
+                c[i] += sg[(size_t)k].bc[i] / (k1 - k0);
+                ca[i] += sg[(size_t)k].ax[i];
+            }
+        }
+        const double cn = std::sqrt(ca[0] * ca[0] + ca[1] * ca[1] + ca[2] * ca[2]);
+        double Rb = 0.0, cosa = 1.0, pl1 = 0.0;
+        for (int k = k0; k < k1 && ok && cn > 0.0; k++) {
+            const Seg& q = sg[(size_t)k];
+            const double dx = q.bc[0] - c[0], dy = q.bc[1] - c[1], dz = q.bc[2] - c[2];
+            Rb = std::max(Rb, std::sqrt(dx * dx + dy * dy + dz * dz) + q.br);
+            cosa = std::min(cosa, (q.ax[0] * ca[0] + q.ax[1] * ca[1] + q.ax[2] * ca[2]) / cn);
+            pl1 = std::max(pl1, q.pl1);
+        }
+        cosa -= 1e-6;  // the float axes and the kernel's dot products
+        ok = ok && cn > 0.0 && cosa > 0.0 && std::isfinite(Rb);
+        for (int i = 0; i < 3; i++) {
+            out[i] = (float)c[i];
+            out[4 + i] = ok ? (float)(ca[i] / cn) : 0.f;
+        }
+        // centre rounded to float: grow R by that, and 1e-5 relative
+        const double cr = 1e-6 * (std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2]));
+        out[3] = ok ? (float)((Rb + cr) * (1.0 + 1e-5) + 1e-5) : INFINITY;
+        out[7] = ok ? (float)cosa : 0.f;
+        out[8] = ok ? (float)std::min(1.0, std::sqrt(std::max(0.0, 1.0 - cosa * cosa)) + 1e-6) : 1.f;
+        out[9] = (float)(pl1 * (1.0 + 1e-6));
+        out[10] = ok ? 0.f : 1.f;
+        out[11] = 0.f;
+    };
+    float* blocks = buf + (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
+    float* groups = blocks + (size_t)SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
+    nblocks = (nseg + SR_TR_BLOCK - 1) / SR_TR_BLOCK;
+    ngroups = (nblocks + SR_TR_GROUP - 1) / SR_TR_GROUP;
+    for (int b = 0; b < nblocks; b++)
+        bound(b * SR_TR_BLOCK, std::min(nseg, (b + 1) * SR_TR_BLOCK), blocks + (size_t)b * SR_TR_BOUND_FLOATS);
+    for (int g = 0; g < ngroups; g++)
+        bound(g * SR_TR_GROUP * SR_TR_BLOCK, std::min(nseg, (g + 1) * SR_TR_GROUP * SR_TR_BLOCK),
+              groups + (size_t)g * SR_TR_BOUND_FLOATS);
+}
+
 // gram_schmidt(mat3(d.xzy, d, d.zxy)), frag:739-753, 764, 789
 void test_ray_frame(V3 d, float* axes9) {
     V3 m0 = v3(d.x, d.z, d.y), m1 = d, m2 = v3(d.z, d.x, d.y);
@@ -354,14 +428,19 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const 
     // {0, 0.5 step_size, 0, 0} (0.5 step_size for RK4, exact; the fast loop
     // loads both with scalar loads of a 32-byte entry). Four padding entries:
     // the step loop loads up to four steps ahead.
-    std::vector<float4> h(2 * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
+    // (geodesic.hip SR_TABLE16: one float4 per step, without the 0.5 step_size)
+#ifndef SR_TABLE16
+#define SR_TABLE16 0
+#endif
+    const size_t stride = SR_TABLE16 ? 1 : 2;
+    std::vector<float4> h(stride * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
     for (int i = 0; i < max_steps; i++) {
         float step = (max_angle - phi) / (float)(max_steps - i);
         phi += step;
         const float c = (float)std::cos((double)phi), sn = (float)std::sin((double)phi);
-        h[2 * (size_t)i] = make_float4(step, step / 6.0f, c, sn);
-        h[2 * (size_t)i + 1] = make_float4(0.f, 0.5f * step, 0.f, 0.f);
+        h[stride * (size_t)i] = make_float4(step, step / 6.0f, c, sn);
+        if (stride == 2) h[2 * (size_t)i + 1] = make_float4(0.f, 0.5f * step, 0.f, 0.f);
     }
     evict_tables(ctx);
     Table& t = ctx->tables[key];
@@ -777,14 +856,14 @@ int sr_create(sr_ctx** out, int hip_device) {
         return SR_E_HIP;
     }
     if (!hip_ok(hipMalloc(&c->d_scene, sizeof(sr_dev_scene))) ||
-        !hip_ok(hipMalloc(&c->d_segs, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float))) ||
+        !hip_ok(hipMalloc(&c->d_segs, (size_t)SR_SEGS_BUF_FLOATS * sizeof(float))) ||
         !hip_ok(hipMalloc(reinterpret_cast<void**>(&c->d_diag), sizeof(int)))) {
         sr_destroy(c);
         return SR_E_NOMEM;
     }
     if (!hip_ok(hipMemsetAsync(c->d_scene, 0, sizeof(sr_dev_scene), c->upload)) ||
         !hip_ok(hipMemsetAsync(c->d_diag, 0, sizeof(int), c->upload)) ||
-        !hip_ok(hipMemsetAsync(c->d_segs, 0, (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS * sizeof(float),
+        !hip_ok(hipMemsetAsync(c->d_segs, 0, (size_t)SR_SEGS_BUF_FLOATS * sizeof(float),
                                c->upload)) ||
         !hip_ok(hipStreamSynchronize(c->upload))) {
         sr_destroy(c);
@@ -990,7 +1069,7 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
     d.tr_flat[13] = t->radius;
     const int n = t->num_curved_points;
     const int nseg = n >= 2 ? n - 1 : 0;
-    std::vector<float> segs((size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS, 0.f);
+    std::vector<float> segs((size_t)SR_SEGS_BUF_FLOATS, 0.f);
     for (int i = 0; i < nseg; i++) {  // frag:777-793
         float* g = segs.data() + (size_t)i * SR_SEG_FLOATS;
         V3 pi = ld(t->curved_points[i]);
@@ -1003,6 +1082,7 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
         g[13] = t->radius;
     }
     d.tr_num_segments = nseg;
+    test_ray_bounds(segs.data(), nseg, t->radius, d.tr_num_blocks, d.tr_num_groups);
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     if (!hip_ok(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice,
                                c->upload)) ||
