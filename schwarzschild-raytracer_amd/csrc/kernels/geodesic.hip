@@ -1956,26 +1956,22 @@ __device__ __forceinline__ float ddu(float u) { return -u * (1.0f - 1.5f * u); }
 // non-subnormal q (the stage values here are never subnormal: DESIGN.md §4);
 // and 2 q is exact, so fma(2, q, a) is the rounding of a + 2 q, as the
 // reference's a + (2. * q).
-// SR_TABLE16: the step table's entry is one float4 {h, h / 6, cos phi, sin
-// phi} (16 bytes: half the scalar loads and SGPRs of the two-float4 entry
-// with 0.5 h), and a + q (0.5 h) is computed as fma(0.5, q h, a): q (0.5 h),
-// (0.5 q) h and 0.5 (q h) are all the rounding of the same product (scaling
-// by 0.5 is exact), and the fused add of the exact 0.5 (q h) rounds once, as
-// the reference's separate add does.
-#ifndef SR_TABLE16
-#define SR_TABLE16 0
-#endif
-#define SR_TBL_STRIDE (SR_TABLE16 ? 1 : 2)  // float4 per step of the step table
-__device__ __forceinline__ float half_step(float a, float q, float h, float hh) {
-    return SR_TABLE16 ? __builtin_fmaf(0.5f, q * h, a) : a + q * hh;
-}
-__device__ __forceinline__ void rk4_step(float u, float du, float h, float hh, float h6, float& un, float& dun) {
+// The step table's entry is one float4 {h, h / 6, cos phi, sin phi} (16
+// bytes), and the reference's a + 0.5 q h (frag:345-349: (0.5 q) h) is
+// computed as fma(0.5, q h, a): (0.5 q) h and 0.5 (q h) are the rounding of
+// the same product (scaling by 0.5 is exact), and the fused add of the exact
+// 0.5 (q h) rounds once, as the reference's separate add does. Against a
+// 32-byte entry that carried 0.5 h: half the scalar loads and SGPRs of the
+// fast loop's prefetch, 0.854 -> 0.843 ms per frame in the pipeline A/B,
+// one frame alone 1.193 -> 1.122 ms (profiles/r05/s4_ab_*.log).
+__device__ __forceinline__ float half_step(float a, float q, float h) { return __builtin_fmaf(0.5f, q * h, a); }
+__device__ __forceinline__ void rk4_step(float u, float du, float h, float h6, float& un, float& dun) {
     const float k1 = du;
     const float l1 = ddu(u);
-    const float k2 = half_step(du, l1, h, hh);
-    const float l2 = ddu(half_step(u, k1, h, hh));
-    const float k3 = half_step(du, l2, h, hh);
-    const float l3 = ddu(half_step(u, k2, h, hh));
+    const float k2 = half_step(du, l1, h);
+    const float l2 = ddu(half_step(u, k1, h));
+    const float k3 = half_step(du, l2, h);
+    const float l3 = ddu(half_step(u, k2, h));
     const float k4 = du + l3 * h;
     const float l4 = ddu(u + k3 * h);
     un = u + h6 * (__builtin_fmaf(2.0f, k3, __builtin_fmaf(2.0f, k2, k1)) + k4);
@@ -2056,7 +2052,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     // {cos phi, sin phi} after step j (step -1: the camera, phi = 0)
     auto phi_cs = [&](int j) -> f2 {
         if (j < 0) return F2(1.0f, 0.0f);
-        const float4 t = tbl[SR_TBL_STRIDE * j];
+        const float4 t = tbl[j];
         return F2(t.z, t.w);
     };
     // materialise the chord of step i - 1 (its end point from r.u, its start
@@ -2149,7 +2145,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const bool any_cm = CULL && __ballot(bcm != 0u);
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
-        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + SR_TBL_STRIDE * i);
+        const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + i);
         float4 e;
         float un, dun, rB;
         uint32_t par;
@@ -2170,9 +2166,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             constexpr int CMV = decltype(cm_tag)::value;
             constexpr bool CM = CMV != 0;
             par = 0;
-            float4 e1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             e = ldc(tp);
-            if (!SR_TABLE16) e1 = ldc(tp + 1);
             f2 pc = CM ? phi_cs(i - 1) : F2(0.0f, 0.0f);  // {cos, sin} phi after the previous step
             const CylDirs<NC> cd = CM ? cyl_dirs(sc, bs) : CylDirs<NC>{};
             const float qh = CM ? ((every || force) ? INFINITY : ball_q(nmin(bm, bs.mh()), bcx, bcy)) : q0;
@@ -2180,11 +2174,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // would also wait for the step table's prefetch (one counter)
             if (CM) __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             float qit = q0;  // CMV 2: the iteration's ball
-            // Step i from entry (e, e1): RK4, the chord-length bound and the
+            // Step i from entry e: RK4, the ball test of its end point and the
             // exit test; true when some lane needs attention (the step is then
             // computed but not applied). k: the step's place in the iteration.
             auto compute = [&](int k) -> bool {
-                rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
+                rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
                 // the end point against the ball (ball_q): a multiply and three FMAs
                 float q = q0;
                 if (CULL && CMV == 1) {
@@ -2209,15 +2203,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #endif
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
             };
-            // apply step i and move to entry (en, en1) of step i + 1
-            auto apply = [&](float4 en, float4 en1) -> bool {
+            // apply step i and move to entry en of step i + 1
+            auto apply = [&](float4 en) -> bool {
                 r.u = un;
                 r.du = dun;
                 if (CMV == 1) rA = rB;
-                tp += SR_TBL_STRIDE;
+                tp += 1;
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
-                e1 = en1;
                 return ++i >= N;
             };
             // FU (SR_FAST_UNROLL) steps per iteration: the entries of steps i + 1
@@ -2228,20 +2221,19 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             // they are issued (sunk to their first use, they would be waited
             // at once).
             for (;;) {
-                constexpr int S = SR_TBL_STRIDE;
-                float4 nx[2 * FU];
+                float4 nx[FU];
 #pragma unroll
-                for (int k = 0; k < S * FU; k++) nx[k] = ldc(tp + S + k);
+                for (int k = 0; k < FU; k++) nx[k] = ldc(tp + 1 + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     if (compute(k)) {
 #pragma unroll
-                        for (int j = S * k; j < S * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = k; j < FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
-                        leave = apply(nx[S * k], S == 2 ? nx[S * k + 1] : e1);
+                        leave = apply(nx[k]);
                     }
                 }
                 if (leave) break;
@@ -2256,32 +2248,28 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // the iterates are the same. Only outward lanes (u < 0.6 falling)
         // coast: u stays finite.
         auto coast = [&]() {
-            constexpr int S = SR_TBL_STRIDE;
-            float4 e1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             e = ldc(tp);
-            if (!SR_TABLE16) e1 = ldc(tp + 1);
             for (;;) {
-                float4 nx[2 * FU];
+                float4 nx[FU];
 #pragma unroll
-                for (int k = 0; k < S * FU; k++) nx[k] = ldc(tp + S + k);
+                for (int k = 0; k < FU; k++) nx[k] = ldc(tp + 1 + k);
                 __builtin_amdgcn_sched_barrier(0);
                 bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
-                    rk4_step(r.u, r.du, e.x, e1.y, e.y, un, dun);  // frag:914-919
+                    rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
                     SR_STAT(0, 1);
                     SR_STAT(11, 1);  // coasting wave-steps
                     SR_STAT(13, __popcll(__ballot(1)));
                     if (__ballot(!(un >= ulo && un <= uhi))) {  // NaN leaves too
 #pragma unroll
-                        for (int j = S * k; j < S * FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
+                        for (int j = k; j < FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
                         leave = true;
                     } else {
                         r.u = un;
                         r.du = dun;
-                        tp += S;
-                        e = nx[S * k];
-                        if (S == 2) e1 = nx[S * k + 1];
+                        tp += 1;
+                        e = nx[k];
                         leave = ++i >= N;
                     }
                 }
@@ -2304,10 +2292,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             if (ie == ick) return upck;
             float u = uck, du = duck;
             for (int j = ick; j < ie - 1; j++) {  // steps ick .. ie - 2
-                const float4 t0 = tbl[SR_TBL_STRIDE * j];
-                const float4 t1 = SR_TABLE16 ? t0 : tbl[2 * j + 1];
+                const float4 t0 = tbl[j];
                 float un2, dun2;
-                rk4_step(u, du, t0.x, t1.y, t0.y, un2, dun2);  // the fast loop's operands
+                rk4_step(u, du, t0.x, t0.y, un2, dun2);  // the fast loop's operands
                 u = un2;
                 du = dun2;
             }

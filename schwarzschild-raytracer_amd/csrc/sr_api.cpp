@@ -424,23 +424,16 @@ int ensure_table(sr_ctx* ctx, int max_steps, int max_revs, hipStream_t s, const 
     }
     // frag:860, 914-915, 925: the angle sequence depends only on the step index
     const float max_angle = 2.0f * (float)max_revs * kPi;
-    // entry i = two float4: {step_size, step_size / 6, cos phi, sin phi} and
-    // {0, 0.5 step_size, 0, 0} (0.5 step_size for RK4, exact; the fast loop
-    // loads both with scalar loads of a 32-byte entry). Four padding entries:
-    // the step loop loads up to four steps ahead.
-    // (geodesic.hip SR_TABLE16: one float4 per step, without the 0.5 step_size)
-#ifndef SR_TABLE16
-#define SR_TABLE16 0
-#endif
-    const size_t stride = SR_TABLE16 ? 1 : 2;
-    std::vector<float4> h(stride * ((size_t)max_steps + 4), make_float4(0.f, 0.f, 0.f, 0.f));
+    // entry i = one float4 {step_size, step_size / 6, cos phi, sin phi} (RK4
+    // forms 0.5 step_size products exactly, geodesic.hip half_step). Four
+    // padding entries: the step loop loads up to four steps ahead.
+    std::vector<float4> h((size_t)max_steps + 4, make_float4(0.f, 0.f, 0.f, 0.f));
     float phi = 0.0f;
     for (int i = 0; i < max_steps; i++) {
         float step = (max_angle - phi) / (float)(max_steps - i);
         phi += step;
         const float c = (float)std::cos((double)phi), sn = (float)std::sin((double)phi);
-        h[stride * (size_t)i] = make_float4(step, step / 6.0f, c, sn);
-        if (stride == 2) h[2 * (size_t)i + 1] = make_float4(0.f, 0.5f * step, 0.f, 0.f);
+        h[(size_t)i] = make_float4(step, step / 6.0f, c, sn);
     }
     evict_tables(ctx);
     Table& t = ctx->tables[key];
