@@ -1300,7 +1300,11 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                                  uint32_t reach, f3 o, f3 d, float seg) {
     Hit best = no_hit();
+#ifdef SR_NO_TR_CULL  // timing experiments only
+    test_ray_hits(sc, segs, best, o, d, seg);
+#else
     test_ray_hits_culled(sc, segs, best, o, d, seg);
+#endif
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
@@ -2335,7 +2339,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // to the origin, then inf / NaN): the exact chord is degenerate (zero
         // length, NaN direction) and the exact tests decide what its NaN
         // arithmetic hits, so every slot is tested (reach below)
+#ifdef SR_NO_DEGEN  // timing experiments only
+        const bool degen = false;
+#else
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
+#endif
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
 #ifdef SR_DEBUG_PX
         if (r.dbg)

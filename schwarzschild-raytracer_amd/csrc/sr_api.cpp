@@ -688,6 +688,9 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
         // (x 1.005: the chord ends' 4e-7 r off the orbital plane, as mu >= SR_MU_PLANAR)
         const double S = ((std::sqrt(3.0) + 3.0) * R * (1.0 + 1e-5) + 1.0) * 1.001 * 1.005;
         fr.xplane_s = S < 1.0e30 ? std::nextafter((float)S, INFINITY) : INFINITY;
+#ifdef SR_XS_FIXED  // timing experiments only: a fixed S_max (not exact for every u_f)
+        fr.xplane_s = SR_XS_FIXED;
+#endif
     }
     fr.percent_black = p->percent_black;
     fr.curved_percentage = p->curved_percentage;
