@@ -2405,7 +2405,15 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
                     const int nl = __popcll(__ballot(event));
                     SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
-#ifdef SR_STATS_TRIG  // measurement only (tools/stats_frame.py --trig): who spends which slot
+#if defined(SR_STATS_STEPHIST)  // measurement only (tools/stats_frame.py --stephist): events by step
+                    {
+                        // events (44 + b) and their triggering lanes (50 + b) by the step
+                        // index's bucket b: < 25, < 100, < 300, < 700, < 1200, the rest
+                        const int bk = i < 25 ? 0 : i < 100 ? 1 : i < 300 ? 2 : i < 700 ? 3 : i < 1200 ? 4 : 5;
+                        SR_STAT(44 + bk, 1);
+                        SR_STAT(50 + bk, nl);
+                    }
+#elif defined(SR_STATS_TRIG)  // measurement only (tools/stats_frame.py --trig): who spends which slot
                     {
                         // lanes whose own budget of slot j ran out (44 + j: orbiting the
                         // photon sphere, 51 + j: the others) and events that re-anchor

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
     ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080], help="render only rows [a, b) (waves alone on the chip)")
     ap.add_argument("--trig", action="store_true", help="an SR_STATS_TRIG build (counters 44..63)")
+    ap.add_argument("--stephist", action="store_true", help="an SR_STATS_STEPHIST build (counters 44..55)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -79,6 +80,12 @@ def main():
              "interval1_triggered", "interval1_reseeded", "interval1_budget_below_0.05", "interval1_cm_events",
              "cm_events"])}
         out["interval1_small_budget_lanes_by_slot"] = [int(hi[23 + j]) for j in range(9)]
+        if args.stephist:  # an SR_STATS_STEPHIST build: events and their lanes by step bucket
+            for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
+                out.pop(k, None)
+            names = ["<25", "25-99", "100-299", "300-699", "700-1199", "1200+"]
+            out["events_by_step"] = dict(zip(names, [int(hi[12 + k]) for k in range(6)]))
+            out["event_lanes_by_step"] = dict(zip(names, [int(hi[18 + k]) for k in range(6)]))
         if args.trig:  # an SR_STATS_TRIG build: counters 44..63 hold the lanes that spent each slot
             for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
                 out.pop(k, None)
