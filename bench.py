@@ -191,8 +191,10 @@ def parse():
     ap.add_argument("--dump-frames", default="",
                     help="directory: rank 0 saves every timed frame as assembled (frame_<f>.npy), for the "
                          "multi-rank parity test; copies are taken after the timed region")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"))
-    ap.add_argument("--pmc-json", default=str(ROOT / "profiles" / "pmc_latest.json"))
+    ap.add_argument("--traffic-json", default="",
+                    help="HBM traffic record (default profiles/traffic_latest[_<variant>].json)")
+    ap.add_argument("--pmc-json", default="",
+                    help="PMC FLOP record (default profiles/pmc_latest[_<variant>].json)")
     return ap.parse_args()
 
 
@@ -848,7 +850,7 @@ def frame_parity(args, W, H, N, quality, use_assets, frame, index):
     if not (args.camera == "static" and use_assets and args.mode == "curved" and args.percent_black < 0):
         out["reason"] = "no oracle fixture for these inputs"
         return out
-    variant = "stress" if args.scene == "stress" else ("testray" if args.test_ray == "on" else "default")
+    variant = scene_variant(args)
     if args.scene == "stress" and args.test_ray == "on":
         out["reason"] = "no oracle fixture for the stress scene with the test ray"
         return out
@@ -875,8 +877,21 @@ def frame_parity(args, W, H, N, quality, use_assets, frame, index):
     return out
 
 
-def load_matching(path, W, H, N, world):
-    """A profiles/*.json record if it was measured on this config and kernel source."""
+def scene_variant(args) -> str:
+    """The scene variant a bench line, its frame-hash fixture and its counter
+    records are keyed by: default, stress (--scene stress) or testray (--test-ray on)."""
+    return "stress" if args.scene == "stress" else ("testray" if args.test_ray == "on" else "default")
+
+
+def profile_record(path: str, kind: str, variant: str) -> Path:
+    """--pmc-json / --traffic-json, or profiles/<kind>_latest[_<variant>].json."""
+    if path:
+        return Path(path)
+    return ROOT / "profiles" / (f"{kind}_latest.json" if variant == "default" else f"{kind}_latest_{variant}.json")
+
+
+def load_matching(path, W, H, N, world, variant="default"):
+    """A profiles/*.json record if it was measured on this config, scene variant and kernel source."""
     p = Path(path)
     if not p.exists():
         return None
@@ -887,6 +902,8 @@ def load_matching(path, W, H, N, world):
     if (rec.get("width"), rec.get("height"), rec.get("max_steps")) != (W, H, N):
         return None
     if rec.get("kernel_sha") not in (None, kernel_sha()):
+        return None
+    if rec.get("variant", "default") != variant:
         return None
     return rec
 
@@ -907,7 +924,8 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
     renders B frames and F launches overlap, `overlap` = kernel_ms / (B x
     ms_per_step)): it is what the rocprofv3 --stats summary of this command
     reports."""
-    pmc = load_matching(args.pmc_json, W, H, N, world)
+    variant = scene_variant(args)
+    pmc = load_matching(profile_record(args.pmc_json, "pmc", variant), W, H, N, world, variant)
     share = sigma_steps_mine / max(1, sigma_steps_frame)  # rank 0's share of the frame's steps
     executed = None
     achieved = None
@@ -921,7 +939,7 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
             valu_issue = (pmc["valu_insts_per_launch"] / per_frame * share * 2.0
                           / (SIMDS * CLOCK_GHZ * 1e9 * ms_per_step * 1e-3))
     traffic = None
-    tr = load_matching(args.traffic_json, W, H, N, world)
+    tr = load_matching(profile_record(args.traffic_json, "traffic", variant), W, H, N, world, variant)
     if tr and world == 1:
         traffic = tr.get("hbm_bytes_per_frame", tr.get("hbm_bytes_per_launch"))
     hbm_bytes = rows_mine * W * 4  # compulsory RGBA8 store; textures stay cache resident

@@ -2317,6 +2317,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         else fast(I0{});
         SR_PT(0);
         if (i >= N) {
+#if defined(SR_STATS_STEPHIST)  // measurement only: recover_up's replayed steps (end of loop)
+            SR_STAT(56, N - 1 - ick);
+            SR_STAT(57, 1);
+#endif
             up = recover_up(N);
             break;
         }
@@ -2327,6 +2331,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         r.i = i;
         r.steps = sbase + i + 1;
         if (un < 0.0f) {
+#if defined(SR_STATS_STEPHIST)  // measurement only: recover_up's replayed steps (u < 0 exit)
+            if (i > ick) SR_STAT(58, i - 1 - ick);
+            SR_STAT(59, 1);
+#endif
             up = recover_up(i);
             settle_prev(i);
             return ST_BG;

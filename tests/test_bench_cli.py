@@ -1,5 +1,6 @@
 """bench.py's command line (driver contract) and its workloads against
 BASELINE.json's configs; no GPU needed."""
+import argparse
 import json
 import re
 import subprocess
@@ -167,10 +168,36 @@ def test_roofline_steps_per_frame_and_launch():
     tex = oracle.TextureSet(sc.skybox(64, 32), sc.default_texture_array()[0])
     launch_steps = sum(int(oracle.render(scene, cam, params, W, H, tex)[2].astype(np.int64).sum()) for _ in range(B))
     frame_steps = launch_steps // B
-    args = argparse.Namespace(pmc_json="/nonexistent", traffic_json="/nonexistent", camera="static")
+    args = argparse.Namespace(pmc_json="/nonexistent", traffic_json="/nonexistent", camera="static",
+                              scene="default", test_ray="off")
     rf = bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None, None)
     assert rf["steps_per_frame"] == frame_steps and rf["frames_per_launch"] == B
     assert rf["steps_per_frame"] * rf["frames_per_launch"] == rf["steps_per_launch"] == launch_steps
     args.camera = "flyby"
     assert bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None,
                                None)["steps_per_launch"] is None
+
+
+def test_counter_records_keyed_by_scene_variant(tmp_path):
+    """A PMC / traffic record counts for a bench line only when it was taken
+    on the same config, kernel source and scene variant (default, stress,
+    testray): the stress and test-ray lines read their own files."""
+    import bench
+
+    args = argparse.Namespace(scene="stress", test_ray="off")
+    assert bench.scene_variant(args) == "stress"
+    assert bench.scene_variant(argparse.Namespace(scene="default", test_ray="on")) == "testray"
+    assert bench.profile_record("", "pmc", "default").name == "pmc_latest.json"
+    assert bench.profile_record("", "traffic", "stress").name == "traffic_latest_stress.json"
+    assert bench.profile_record(str(tmp_path / "x.json"), "pmc", "stress") == tmp_path / "x.json"
+    rec = {"width": 640, "height": 360, "max_steps": 1000, "kernel_sha": bench.kernel_sha(), "variant": "stress"}
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps(rec))
+    assert bench.load_matching(p, 640, 360, 1000, 1, "stress") == rec
+    assert bench.load_matching(p, 640, 360, 1000, 1, "default") is None
+    assert bench.load_matching(p, 640, 360, 1000, 1, "testray") is None
+    assert bench.load_matching(p, 1920, 1080, 2000, 1, "stress") is None
+    del rec["variant"]  # records from before the variant key: the default scene
+    p.write_text(json.dumps(rec))
+    assert bench.load_matching(p, 640, 360, 1000, 1) == rec
+    assert bench.load_matching(p, 640, 360, 1000, 1, "stress") is None

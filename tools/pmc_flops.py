@@ -99,6 +99,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--variant", default="default", choices=["default", "stress", "testray"],
+                    help="the bench's scene variant (--scene stress / --test-ray on)")
     ap.add_argument("--out", default=str(ROOT / "profiles" / "pmc_latest.json"))
     ap.add_argument("--source", default="")
     args = ap.parse_args()
@@ -138,6 +140,7 @@ def main():
         "width": args.width,
         "height": args.height,
         "max_steps": args.max_steps,
+        "variant": args.variant,
         "grid_threads": grid,
         "dispatches_averaged": max(n.values()) if n else 0,
         "frames_per_launch": B,

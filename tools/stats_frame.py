@@ -86,6 +86,8 @@ def main():
             names = ["<25", "25-99", "100-299", "300-699", "700-1199", "1200+"]
             out["events_by_step"] = dict(zip(names, [int(hi[12 + k]) for k in range(6)]))
             out["event_lanes_by_step"] = dict(zip(names, [int(hi[18 + k]) for k in range(6)]))
+            out["recover_up"] = {"end_replayed_wave_steps": int(hi[24]), "end_exits": int(hi[25]),
+                                 "neg_u_replayed_wave_steps": int(hi[26]), "neg_u_exits": int(hi[27])}
         if args.trig:  # an SR_STATS_TRIG build: counters 44..63 hold the lanes that spent each slot
             for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
                 out.pop(k, None)

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--max-steps", type=int, default=2000)
+    ap.add_argument("--variant", default="default", choices=["default", "stress", "testray"],
+                    help="the bench's scene variant (--scene stress / --test-ray on)")
     a = ap.parse_args()
     import bench
 
@@ -37,7 +39,7 @@ def main():
     rec = {
         "kernel": "sr_integrate_kernel<true, false, NB>",
         "kernel_sha": bench.kernel_sha(),
-        "width": a.width, "height": a.height, "max_steps": a.max_steps,
+        "width": a.width, "height": a.height, "max_steps": a.max_steps, "variant": a.variant,
         "fetch_bytes_raw": fetch, "fetch_bytes_x2_bound": 2 * fetch, "write_bytes": write,
         "hbm_bytes_per_launch": fetch + write,
         "frames_per_launch": B,
