@@ -596,9 +596,6 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #ifndef SR_CM_ITER  // the cylinder-plane fast loop tests the chord direction once per iteration (integrate)
 #define SR_CM_ITER 1
 #endif
-#ifndef SR_UP_CHUNK  // fast-loop steps between recover_up checkpoints (0: the loop's entry only)
-#define SR_UP_CHUNK 0
-#endif
 #ifndef SR_COAST  // the RK4-only fast loop of waves whose every budget is +inf (integrate)
 #define SR_COAST 1
 #endif
@@ -2156,40 +2153,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         float4 e;
         float un, dun, rB;
         uint32_t par;
-        // The fast loop does not carry `up` (u after step i - 2): the copy
-        // cost a register move per step in its rotation (42.3 -> 41.7 VALU
-        // per step). The two exits that need it - u < 0 (the previous chord,
-        // frag:921-922) and the end of the loop - recompute it from the
-        // loop's entry state with the same RK4 steps (bit-identical).
-        int ick = i;
-        float uck = r.u, duck = r.du, upck = up;
-        // SR_UP_CHUNK > 0: every SR_UP_CHUNK steps the loops stop at a scalar
-        // limit (the same compare as the end-of-loop one) and take a new
-        // checkpoint, so a replay runs at most that many steps; the limit's
-        // apply keeps the u it overwrote (upl) for the checkpoint's `up`
-        int ilim = SR_UP_CHUNK > 0 ? min(N, i + SR_UP_CHUNK) : N;
-        float upl = 0.0f;
-        auto checkpoint = [&]() -> bool {  // false at the end of the loop
-            if (SR_UP_CHUNK <= 0 || i >= N) return false;
-            ick = i;
-            uck = r.u;
-            duck = r.du;
-            upck = upl;
-            ilim = min(N, i + SR_UP_CHUNK);
-            return true;
-        };
-        auto recover_up = [&](int ie) -> float {  // u after step ie - 2
-            if (ie == ick) return upck;
-            float u = uck, du = duck;
-            for (int j = ick; j < ie - 1; j++) {  // steps ick .. ie - 2
-                const float4 t0 = tbl[j];
-                float un2, dun2;
-                rk4_step(u, du, t0.x, t0.y, un2, dun2);  // the fast loop's operands
-                u = un2;
-                du = dun2;
-            }
-            return u;
-        };
         // Three versions of the loop: without a lane whose orbital plane nearly
         // contains a budgeted cylinder's axis (the usual case, CMV 0) the
         // limit is fixed and there is no direction test; with one, the chord's
@@ -2246,18 +2209,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             };
             // apply step i and move to entry en of step i + 1
             auto apply = [&](float4 en) -> bool {
-                const float uo = r.u;
                 r.u = un;
                 r.du = dun;
                 if (CMV == 1) rA = rB;
                 tp += 1;
                 if (CM) pc = F2(e.z, e.w);
                 e = en;
-                if (++i >= ilim) {
-                    upl = uo;  // u after step i - 2: a checkpoint's `up`
-                    return true;
-                }
-                return false;
+                return ++i >= N;
             };
             // FU (SR_FAST_UNROLL) steps per iteration: the entries of steps i + 1
             // .. i + FU are loaded together at its top (the table
@@ -2271,20 +2229,18 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #pragma unroll
                 for (int k = 0; k < FU; k++) nx[k] = ldc(tp + 1 + k);
                 __builtin_amdgcn_sched_barrier(0);
-                bool leave = false, exit_ = false;
+                bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     if (compute(k)) {
 #pragma unroll
                         for (int j = k; j < FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
-                        leave = exit_ = true;
+                        leave = true;
                     } else {
                         leave = apply(nx[k]);
                     }
                 }
-                if (leave) {
-                    if (exit_ || !checkpoint()) break;
-                }
+                if (leave) break;
             }
         };
         // Coasting: when every lane's limit is +inf (escaping rays that have
@@ -2302,7 +2258,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
 #pragma unroll
                 for (int k = 0; k < FU; k++) nx[k] = ldc(tp + 1 + k);
                 __builtin_amdgcn_sched_barrier(0);
-                bool leave = false, exit_ = false;
+                bool leave = false;
 #pragma unroll
                 for (int k = 0; k < FU && !leave; k++) {
                     rk4_step(r.u, r.du, e.x, e.y, un, dun);  // frag:914-919
@@ -2312,28 +2268,41 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     if (__ballot(!(un >= ulo && un <= uhi))) {  // NaN leaves too
 #pragma unroll
                         for (int j = k; j < FU; j++) asm volatile("; keep %0" ::"s"(nx[j].x));
-                        leave = exit_ = true;
+                        leave = true;
                     } else {
-                        const float uo = r.u;
                         r.u = un;
                         r.du = dun;
                         tp += 1;
                         e = nx[k];
-                        if (++i >= ilim) {
-                            upl = uo;
-                            leave = true;
-                        }
+                        leave = ++i >= N;
                     }
                 }
-                if (leave) {
-                    if (exit_ || !checkpoint()) break;
-                }
+                if (leave) break;
             }
             // the state the full loop leaves: step i's radius, no charge (every budget is +inf)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
             par = 0;
             vb = -1.0f;  // inside every (infinite) budget
+        };
+        // The fast loop does not carry `up` (u after step i - 2): the copy
+        // cost a register move per step in its rotation (42.3 -> 41.7 VALU
+        // per step). The two exits that need it - u < 0 (the previous chord,
+        // frag:921-922) and the end of the loop - recompute it from the
+        // loop's entry state with the same RK4 steps (bit-identical).
+        const int ick = i;
+        const float uck = r.u, duck = r.du, upck = up;
+        auto recover_up = [&](int ie) -> float {  // u after step ie - 2
+            if (ie == ick) return upck;
+            float u = uck, du = duck;
+            for (int j = ick; j < ie - 1; j++) {  // steps ick .. ie - 2
+                const float4 t0 = tbl[j];
+                float un2, dun2;
+                rk4_step(u, du, t0.x, t0.y, un2, dun2);  // the fast loop's operands
+                u = un2;
+                du = dun2;
+            }
+            return u;
         };
         // CMV 2 needs every lane in a u window (u <= SR_BH_U2 at applied steps)
         // and the three chords' turning 1.5 SR_BH_U2 x 1.01 x 3 max_dphi within 0.05
