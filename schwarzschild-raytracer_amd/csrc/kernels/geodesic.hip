@@ -239,7 +239,11 @@ __device__ __forceinline__ bool cyl_test(f3 o, f3 d, f3 pos, const m3& A, float 
 // any order (or skipped) with the same winner.
 enum { KEY_BH = 0, KEY_TR_FLAT = 1, KEY_TR_CURVED0 = 2, KEY_OBJ0 = 2 + SR_MAX_POINTS };
 
-__device__ __forceinline__ void consider(Hit& best, bool hit, f3 p, f3 o, int slot, int face, int key) {
+// p by reference: callers pass the point their own test argument writes
+// (consider(best, test(..., p), p, ...)), and the order in which a call's
+// arguments are evaluated is unspecified, so a by-value copy could be taken
+// before the test ran.
+__device__ __forceinline__ void consider(Hit& best, bool hit, const f3& p, f3 o, int slot, int face, int key) {
     if (!hit) return;
     float dist = len(p - o);
     if (best.slot == SLOT_NONE || dist < best.dist || (dist == best.dist && key < best.key)) {
@@ -2618,10 +2622,6 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 // instantiation; 5 (96 VGPRs) for the general one (8 slots, 3 cylinders),
 // whose event path then keeps every value in registers (at 6 it spilled 9 in
 // the reseed path), its 6.5 KiB of LDS per wave allowing 24 waves per CU
-#ifndef SR_BATCH_WAVES  // the small instantiation's waves per SIMD for batched launches (0: as single frames)
-#define SR_BATCH_WAVES 7
-#endif
-constexpr int kBatchWaves = SR_BATCH_WAVES > 0 ? SR_BATCH_WAVES : SR_MIN_WAVES_PER_EU;
 constexpr int sr_integrate_waves(int nb, int nc) {
     return nb > SR_NB_GENERAL ? SR_LARGE_WAVES_PER_EU
                               : (nb > SR_NB_SMALL || nc > SR_NC_SMALL) ? SR_GENERAL_WAVES_PER_EU : SR_MIN_WAVES_PER_EU;
@@ -2662,10 +2662,8 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // sr_launch_geodesic picks SR_NB_SMALL when it suffices: the default scene
 // has six, and phase 1 of an event runs over every slot of the capacity).
 // NC: budgeted cylinders it handles (SR_NC_SMALL with SR_NB_SMALL).
-// WV: waves per SIMD to build for (0: sr_integrate_waves(NB, NC)).
-template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS,
-          int WV = 0>
-__global__ __launch_bounds__(SR_WG, WV ? WV : sr_integrate_waves(NB, NC)) void sr_integrate_kernel(
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS>
+__global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
     size_t ps_n, int* __restrict__ count, const int* __restrict__ order, int* __restrict__ cost) {
@@ -3040,10 +3038,6 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (small && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
         hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, 2, SR_NC_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
-                           dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
-    else if (small && B > 1 && SR_BATCH_WAVES > 0)  // batched launches: throughput
-        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, SR_FAST_UNROLL, SR_NC_SMALL, kBatchWaves>),
-                           dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     else if (small)
         hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, SR_FAST_UNROLL, SR_NC_SMALL>),
