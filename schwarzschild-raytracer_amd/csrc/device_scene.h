@@ -228,6 +228,22 @@ typedef struct {
     // |o|_1 + len + 1 of every chord from inside the u_f sphere to within 2 R
     // (geodesic.hip budget_frame's orbital-plane exclusion); +inf when u_f <= 0
     float xplane_s;
+    // the inner black-hole window's upper bounds on u (geodesic.hip
+    // SR_BH_WINDOW2): out_dip / (1 + SR_BH_G2) for every lane (chords stay
+    // SR_BH_G2 off the shell, above the discriminant's error at tangency),
+    // and out_dip / (1 + SR_BH_G3) for steep falling lanes (E >= SR_BH_E_MIN)
+    // when max_dphi <= SR_BH_S_DPHI (else bh_u2); both rounded down
+    float bh_u2, bh_u3;
 } sr_dev_frame;
+
+// the inner black-hole window's margins (sr_api.cpp build_frame, geodesic.hip)
+#define SR_BH_G2 1.5e-3
+#define SR_BH_G3 6.0e-5
+#define SR_BH_S_DPHI 0.0132f
+#define SR_BH_E_MIN 0.1452f
+// u at r = 1 - 1e-3 and r = 1 - SR_BH_G3, rounded up: an end point past these
+// (with the chord's start in the window) has certainly entered the shell
+#define SR_BH_UIN2 1.00100112f
+#define SR_BH_UIN3 1.00006008f
 
 #endif

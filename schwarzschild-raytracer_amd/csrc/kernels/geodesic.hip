@@ -94,6 +94,9 @@ struct Tex {
     const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
+#ifdef SR_STATS_NEARBH
+__device__ int sr_nearbh_prints;
+#endif
 // budget slots 0 .. 8 have their own counters in measurement builds
 #define SR_STATS_SLOTS 9
 #ifdef SR_STATS
@@ -650,20 +653,43 @@ struct BudgetLayout {
 #define SR_BH_U 0.986f      // u at r = 1.01420
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
 // The inner window (SR_BH_WINDOW2): chords whose two ends both lie at r in
-// [1.00402, 1.1] (u in [SR_BH_ULO2, SR_BH_U2]) with a step angle below 0.063
+// [1.00402, 1.1] (u in [SR_BH_ULO2, 0.996]) with a step angle below 0.063
 // (out_dip > SR_BH_DIP2) stay at least 1.00402 x 0.9995 = 1.00352 from the
 // origin. sphere_test computes their discriminant within 12 eps (|o|^2 + 1)
 // <= 1.6e-6 (|o| <= 1.1), so a root it accepts lies within sqrt(1.6e-6) =
 // 1.26e-3 of a true root (near tangency; less elsewhere), while the segment
 // ends at least 3.5e-3 from the sphere along the line: none is accepted. A
 // lane there needs no distance budget for the hole either; the step loop
-// exits on u > SR_BH_U2 or u < SR_BH_ULO2 (climbing past r = 1.1; the u_f
+// exits on u > 0.996 or u < SR_BH_ULO2 (climbing past r = 1.1; the u_f
 // compare, per lane). Rays falling in crossed the band r < 1.0142 with an
 // event on every step (their distance budget was below one step).
 #ifndef SR_BH_WINDOW2
 #define SR_BH_WINDOW2 1
 #endif
-#define SR_BH_U2 0.996f       // u at r = 1.004016
+// Round 5: the window's upper bound follows the frame's step angle instead
+// of r = 1.004 (sr_dev_frame.bh_u2 = out_dip / (1 + SR_BH_G2)): a chord with
+// both ends at u <= bh_u2 stays min(rA, rB) out_dip >= 1 + SR_BH_G2 = 1.0015
+// from the origin (less the end points' 2.2e-6), above the 1.26e-3 a root
+// can move at tangency. Falling lanes steep enough (the orbit's invariant E =
+// u'^2 + u^2 - u^3 >= SR_BH_E_MIN at the window's anchor, and max_dphi <=
+// SR_BH_S_DPHI) get bh_u3 = out_dip / (1 + SR_BH_G3), 6e-5 off the shell:
+// u'' > 0 for u > 2/3, so u' only grows on the way in (each RK4 stage adds a
+// positive term), u' >= sqrt(E - u^2 (1 - u)) >= 0.367 once u >= 0.99 (E
+// drifts by < 3e-5 over the window), and a chord from u_A to u_B >= 0.998
+// rises u_B - u_A >= 0.367 dphi (u_A >= 0.99) or >= 0.008 >= 0.6 dphi (u_A <
+// 0.99): its line passes within rho^2 <= rA rB / (1 + (u_B - u_A)^2 / (u_A
+// u_B dphi^2)) <= 0.9 of the origin (2 (1 - cos) >= sin^2 in the chord's
+// length), so sphere_test's discriminant is >= 0.1 and its roots move by at
+// most 1.6e-6 / 0.316 + 3e-7 < 6e-6, ten times below the clearance. The
+// same bounds make a crossing certain (the integrate slow path): a chord from
+// inside the window (u_A <= uhi) to u_B >= SR_BH_UIN3 (steep lanes; inside
+// r = 1 - 6e-5) or >= SR_BH_UIN2 (any lane: inside 1 - 1e-3, so the line
+// passes within 0.999 of the origin, the discriminant is >= 2e-3 and a root
+// moves by < 4e-5) has its entry root at least 5.8e-5 from both ends: the
+// computed lambda1 is positive, below the length, and the smaller positive
+// root. With the lane's other slots covered by its ball (vb < 0, no forced
+// chord, no per-chord objects) the hole is the closest hit: ST_BH (the shade
+// kernel reads its status and step count only) without the event.
 #define SR_BH_ULO2 0.90910f   // u at r = 1.09999
 #define SR_BH_RWIN2 1.00403f  // an anchor beyond this radius (by perr) ...
 #define SR_BH_RMAX2 1.0999f   // ... and within this one starts an inner window
@@ -702,8 +728,8 @@ struct Budget {
     //   mh  min_k of the cylinders' slab budgets H[k] (E[SLAB0 + k]): the bound
     //       that covers chords nearly parallel to an axis
     //   cm  budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
-    //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; SR_BH_U2:
-    //       the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo_of())
+    //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; bh_u2 /
+    //       bh_u3: the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo_of())
     __device__ __forceinline__ float ld(int row) const { return E[row * SR_E_STRIDE]; }
     __device__ __forceinline__ void st(int row, float v) const { E[row * SR_E_STRIDE] = v; }
     __device__ __forceinline__ float T() const { return ld(L::BT); }
@@ -727,7 +753,9 @@ struct Budget {
     }
     __device__ __forceinline__ float uhi() const { return ld(L::BUHI); }
     __device__ __forceinline__ void setUhi(float v) const { st(L::BUHI, v); }
-    static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return uhi == SR_BH_U2 ? SR_BH_ULO2 : u_f; }
+    // the inner window (uhi in (SR_BH_U, 1): sr_dev_frame.bh_u2 / bh_u3)
+    static __device__ __forceinline__ bool inner(float uhi) { return uhi > SR_BH_U && uhi < 1.0f; }
+    static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return inner(uhi) ? SR_BH_ULO2 : u_f; }
 #ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
     int fires;
 #endif
@@ -815,7 +843,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 
 template <class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
-                                            bool outward, float dip, bool bh_ok, bool falling, float xs) {
+                                            bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.setT(0.0f);
@@ -839,7 +867,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         }
         if (SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a > SR_BH_RWIN2 && a < SR_BH_RMAX2 && (falling || !(a > SR_BH_RWIN))) {
             e = INFINITY;
-            uhi = SR_BH_U2;
+            uhi = u2w;
         }
         bs.setUhi(uhi);
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
@@ -1017,7 +1045,8 @@ template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
-                                                 bool falling, bool par_recompute, float u_f) {
+                                                 bool falling, bool par_recompute, float u_f, float u2, float u3,
+                                                 bool steep) {
     constexpr int NB = BS::NB, NC = BS::NC;
     constexpr int NS = NB + 1;  // the slots this kernel instantiation handles (sc->num_budget <= NB)
     const int nb = sc->num_budget;
@@ -1144,7 +1173,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a - perr > SR_BH_RWIN2 && a + perr < SR_BH_RMAX2 &&
                               (falling || !win1);
             const bool win = win1 || win2;
-            bs.setUhi(win2 ? SR_BH_U2 : win1 ? SR_BH_U : INFINITY);
+            bs.setUhi(win2 ? (steep ? u3 : u2) : win1 ? SR_BH_U : INFINITY);
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
@@ -1796,6 +1825,9 @@ struct Ray {
 #ifdef SR_PROF
     unsigned* prof;  // the wave's 8 section accumulators in LDS
 #endif
+#ifdef SR_STATS_NEARBH
+    int px, py;
+#endif
 #ifdef SR_STATS
     int ev, mat;  // budget events, exact chords (measurement builds)
     int rc[SR_STATS_SLOTS];
@@ -2035,7 +2067,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s);
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -2086,6 +2118,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     int i = r.i;
 #ifdef SR_STATS
     int last_ev = i;
+    int near_run = 0;
 #endif
 #ifdef SR_PROF
     unsigned prof_t_ = (unsigned)clock64();
@@ -2162,10 +2195,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // limit is fixed and there is no direction test; with one, the chord's
         // direction is tested on every step (CMV 1) or, when every lane is in
         // a black-hole u window, on the first step of each three-step
-        // iteration only (CMV 2, SR_CM_ITER): with u <= SR_BH_U2 at every
+        // iteration only (CMV 2, SR_CM_ITER): with u <= uhi < 1 at every
         // applied step's ends the orbit's tangent turns by at most 1.5 u per
         // radian of phi (dpsi/dphi = 1.5 u^3 / (u^2 + u'^2)), so the next two
-        // chords lie within 4.53 max_dphi of the tested one's direction, below
+        // chords lie within 4.55 max_dphi of the tested one's direction, below
         // the 0.0555 rad between chord_parallel's threshold (|d_perp|^2 <
         // 2 SR_BUDGET_DPMIN, direction known to 0.004) and the margin's
         // (|d_perp|^2 >= SR_BUDGET_DPMIN). The exit step's chord is tested
@@ -2308,10 +2341,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             }
             return u;
         };
-        // CMV 2 needs every lane in a u window (u <= SR_BH_U2 at applied steps)
-        // and the three chords' turning 1.5 SR_BH_U2 x 1.01 x 3 max_dphi within 0.05
-        const bool cm_iter = SR_CM_ITER && any_cm && !__ballot(!(uhi <= SR_BH_U2)) &&
-                             4.53f * fr.max_dphi < 0.05f;
+        // CMV 2 needs every lane in a u window (u <= uhi < 1 at applied steps)
+        // and the three chords' turning 1.5 x 1.01 x 3 max_dphi within 0.05
+        const bool cm_iter = SR_CM_ITER && any_cm && !__ballot(!(uhi < 1.0f)) &&
+                             4.55f * fr.max_dphi < 0.05f;
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
@@ -2344,7 +2377,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return ST_BG;
         }
         // the chord left the black hole's u window (or the inner one outward)
-        const bool bhx = un > uhi || (un < SR_BH_ULO2 && uhi == SR_BH_U2);
+        const bool bhx = un > uhi || (un < SR_BH_ULO2 && BS::inner(uhi));
         // a chord ending beyond 2 / u_f, which the orbital-plane exclusions do
         // not cover (budget_frame): an event that forces them (budget_event)
         // a ray through the singularity (u past 1e30: its chord points round
@@ -2357,6 +2390,15 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
 #endif
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
+#ifndef SR_BH_CROSS
+#define SR_BH_CROSS 1
+#endif
+        // a certain crossing of the shell from inside the inner window (its
+        // proof at SR_BH_WINDOW2): the hole is this chord's closest hit
+        if (RECORD && CULL && SR_BH_CROSS && !every && __ballot(BS::inner(uhi) && un >= SR_BH_UIN3)) {
+            const float uin = (uhi == fr.bh_u3 && fr.bh_u3 != fr.bh_u2) ? SR_BH_UIN3 : SR_BH_UIN2;
+            if (BS::inner(uhi) && un >= uin && un < 1.0e30f && vb < 0.0f && !force) return ST_BH;
+        }
 #ifdef SR_DEBUG_PX
         if (r.dbg)
             printf("[%d] slow i %d u %.9g un %.9g du %.9g vb %g bhx %d ev %d uhi %g E0 %g T %g m %g excl %x\n", r.dbg, i,
@@ -2424,6 +2466,53 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                         const int bk = i < 25 ? 0 : i < 100 ? 1 : i < 300 ? 2 : i < 700 ? 3 : i < 1200 ? 4 : 5;
                         SR_STAT(44 + bk, 1);
                         SR_STAT(50 + bk, nl);
+                    }
+#elif defined(SR_STATS_NEAR)
+#ifdef SR_STATS_NEARBH
+#define SR_STATS_NEARBH_ON 1
+#else
+#define SR_STATS_NEARBH_ON 0
+#endif
+                    // measurement only (tools/stats_frame.py --near): back-to-back events
+                    {
+                        // slots some lane has spent at this event (bit j), by interval 1 (44..46:
+                        // one, two, three or more slots) and longer (47..49); runs of consecutive
+                        // interval-1 events, recorded when a longer interval ends one (50..54:
+                        // 1, 2-3, 4-7, 8-15, 16+); interval-1 events spending one slot, by slot (55..61)
+                        const float Tt = bs.T();
+                        uint32_t sm = 0;
+                        for (int j = 0; j < 7; j++) {
+                            const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
+                            if (__ballot(!(Tt < ej))) sm |= 1u << j;
+                        }
+                        const int ns = __popc(sm);
+#ifndef SR_STATS_NEARBH
+                        SR_STAT((iv <= 1 ? 44 : 47) + (ns <= 1 ? 0 : ns == 2 ? 1 : 2), 1);
+#endif
+                        if (iv <= 1) {
+                            near_run++;
+#ifdef SR_STATS_NEARBH  // the lanes spending the black hole's slot alone at interval 1, by u and sign of u'
+                            if (sm == 1u) {
+                                const bool own = !(Tt < bs.E[0]);
+                                const float uu = r.u;
+                                const int ub = uu < 0.986f ? 0 : uu < 0.996f ? 1 : uu < 1.0f ? 2 : uu < 1.01f ? 3 : uu < 1.5f ? 4 : 5;
+                                for (int k = 0; k < 6; k++) {
+                                    SR_STAT(44 + k, __popcll(__ballot(own && ub == k && r.du > 0.0f)));
+                                    SR_STAT(50 + k, __popcll(__ballot(own && ub == k && !(r.du > 0.0f))));
+                                }
+                                // a few lanes in long runs: where they are
+                                if (near_run == 40 && own && (int)__lane_id() == __builtin_ctzll(__ballot(own)) &&
+                                    atomicAdd(&sr_nearbh_prints, 1) < 12)
+                                    printf("nearbh px %d py %d i %d u %.9g du %.9g up %.9g T %g E0 %g m %g uhi %g\n", r.px, r.py,
+                                           i, r.u, r.du, up, Tt, bs.E[0], bs.m(), bs.uhi());
+                            }
+#else
+                            if (ns == 1) SR_STAT(55 + __builtin_ctz(sm), 1);
+#endif
+                        } else if (near_run > 0) {
+                            if (!SR_STATS_NEARBH_ON) SR_STAT(50 + (near_run <= 1 ? 0 : near_run <= 3 ? 1 : near_run <= 7 ? 2 : near_run <= 15 ? 3 : 4), 1);
+                            near_run = 0;
+                        }
                     }
 #elif defined(SR_STATS_TRIG)  // measurement only (tools/stats_frame.py --trig): who spends which slot
                     {
@@ -2507,9 +2596,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
+                // the inner window's bound for this lane: steep falling lanes get bh_u3
+                const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
-                                     fr.u_f);
+                                     fr.u_f, fr.bh_u2, fr.bh_u3, steep);
                 if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
                 SR_PT(6);
 #ifdef SR_STATS
@@ -2715,6 +2806,10 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         Ray r;
         Hit hit;
         int st = init_pixel(fr, fr.cam[frame], q, r);
+#ifdef SR_STATS_NEARBH
+        r.px = q.px;
+        r.py = q.py;
+#endif
 #ifdef SR_DEBUG_PX
         r.dbg = (q.px == SR_DEBUG_PX && q.py == SR_DEBUG_PY) ? 1 : 0;
         if (r.dbg) printf("[1] init st %d u %.9g du %.9g\n", st, r.u, r.du);

@@ -710,6 +710,11 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
         const double dphi = (double)fr.max_angle / (p->max_steps > 0 ? p->max_steps : 1);
         fr.out_dip = (float)(1.0 - dphi * dphi / 8.0 - 1e-6);
         fr.max_dphi = std::nextafter((float)std::sqrt(8.0 * (1.0 - (double)fr.out_dip)), INFINITY);
+        // the inner black-hole window's bounds (geodesic.hip SR_BH_WINDOW2)
+        fr.bh_u2 = std::nextafter((float)((double)fr.out_dip / (1.0 + SR_BH_G2)), 0.0f);
+        fr.bh_u3 = fr.max_dphi <= SR_BH_S_DPHI
+                       ? std::nextafter((float)((double)fr.out_dip / (1.0 + SR_BH_G3)), 0.0f)
+                       : fr.bh_u2;
     }
     fr.split_tiles = ctx->split_tiles;
     fr.split_log2 = ctx->split_log2;
