@@ -691,8 +691,9 @@ struct BudgetLayout {
 // chord, no per-chord objects) the hole is the closest hit: ST_BH (the shade
 // kernel reads its status and step count only) without the event.
 #define SR_BH_ULO2 0.90910f   // u at r = 1.09999
-#define SR_BH_RWIN2 1.00403f  // an anchor beyond this radius (by perr) ...
-#define SR_BH_RMAX2 1.0999f   // ... and within this one starts an inner window
+// an anchor within this radius (by perr) and at u <= the window's bound
+// (budget_event: (a - perr) uw > 1) starts an inner window
+#define SR_BH_RMAX2 1.0999f
 #define SR_BH_DIP2 0.9995f
 #define SR_BH_DIP 0.9935f   // 1.0142 x 0.9935 = 1.0076
 
@@ -865,7 +866,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
             e = INFINITY;
             uhi = SR_BH_U;
         }
-        if (SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a > SR_BH_RWIN2 && a < SR_BH_RMAX2 && (falling || !(a > SR_BH_RWIN))) {
+        if (SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a * u2w > 1.000001f && a < SR_BH_RMAX2 && (falling || !(a > SR_BH_RWIN))) {
             e = INFINITY;
             uhi = u2w;
         }
@@ -1170,10 +1171,13 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         if (j == 0) {
             // beyond the band: the u window instead of a distance budget
             const bool win1 = SR_BH_WINDOW && bh_ok && a - perr > SR_BH_RWIN;
-            const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && a - perr > SR_BH_RWIN2 && a + perr < SR_BH_RMAX2 &&
-                              (falling || !win1);
+            // the inner window from an anchor already inside its bound (u <= uw:
+            // a re-anchor near the shell, e.g. by another lane's event, keeps it)
+            const float uw = steep ? u3 : u2;
+            const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && (a - perr) * uw > 1.000001f &&
+                              a + perr < SR_BH_RMAX2 && (falling || !win1);
             const bool win = win1 || win2;
-            bs.setUhi(win2 ? (steep ? u3 : u2) : win1 ? SR_BH_U : INFINITY);
+            bs.setUhi(win2 ? uw : win1 ? SR_BH_U : INFINITY);
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
@@ -2501,10 +2505,11 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                                     SR_STAT(50 + k, __popcll(__ballot(own && ub == k && !(r.du > 0.0f))));
                                 }
                                 // a few lanes in long runs: where they are
-                                if (near_run == 40 && own && (int)__lane_id() == __builtin_ctzll(__ballot(own)) &&
-                                    atomicAdd(&sr_nearbh_prints, 1) < 12)
-                                    printf("nearbh px %d py %d i %d u %.9g du %.9g up %.9g T %g E0 %g m %g uhi %g\n", r.px, r.py,
-                                           i, r.u, r.du, up, Tt, bs.E[0], bs.m(), bs.uhi());
+                                if (near_run >= 8 && own && (int)__lane_id() == __builtin_ctzll(__ballot(own)) &&
+                                    atomicAdd(&sr_nearbh_prints, 1) < 24)
+                                    printf("nearbh px %d py %d i %d run %d u %.9g du %.9g up %.9g T %g E0 %g m %g uhi %g E %g\n",
+                                           r.px, r.py, i, near_run, r.u, r.du, up, Tt, bs.E[0], bs.m(), bs.uhi(),
+                                           r.du * r.du + r.u * r.u * (1.0f - r.u));
                             }
 #else
                             if (ns == 1) SR_STAT(55 + __builtin_ctz(sm), 1);
