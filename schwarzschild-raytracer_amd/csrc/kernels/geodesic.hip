@@ -510,7 +510,19 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     return (Lc > 0.0f && f > 0.0f) ? Lc * f * 0.998f : 0.0f;
 }
 // slot j >= 1 for an outward lane at distance a (cyl_par: bs.cm's bit for a budgeted cylinder)
+// Round 5: a cylinder is excluded for outward lanes whose orbital plane can
+// hold a chord nearly parallel to its axis (bs.cm) too. Its distance budget
+// covers only chords with |d_perp|^2 >= SR_BUDGET_DPMIN (sl.qk's margin);
+// nearly parallel ones are the slab budget's (the cylinder-plane fast loop's
+// ball min(m, mh) and budget_event's forced bit), which the exclusion leaves
+// alone. Escaping lanes of the frame's centre column (orbital planes through
+// the cylinder's axis) re-anchored its 32-unit window every step or two on
+// their way out to u_f: the slowest waves' most frequent event.
+#ifndef SR_OUT_CYL_CM
+#define SR_OUT_CYL_CM 1
+#endif
 __device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par, float a, float dip) {
+    if (SR_OUT_CYL_CM) cyl_par = false;
     if (sl.type == SR_OBJECT_PLANE || (sl.type == SR_OBJECT_CYLINDER && (cyl_par || !(sl.x1 > 0.0f)))) return false;
     return outward_clear(sl.cn, sl.br, sl.mu, sl.type == SR_OBJECT_CYLINDER ? sl.qk : 0.0f, sl.pl1, a, dip);
 }
@@ -1118,6 +1130,9 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             if (__ballot((forced >> j) & 1u)) spent |= 1u << j;
     }
     spent &= (2u << nb) - 1u;
+    // uniform by construction (ballots); said so, so that the slot records
+    // below stay scalar loads in every build (pin_slot's SGPR constraints)
+    spent = __builtin_amdgcn_readfirstlane(spent);
     SR_PTB(20);
 #ifdef SR_PROF
     {
@@ -2601,12 +2616,48 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
+#ifdef SR_DEBUG_PX  // the debug lane's wave: what each event spends and looks ahead at
+                if (__ballot(r.dbg)) {
+                    uint32_t sm = 0, lm = 0;
+                    const float Tt = bs.T();
+                    for (int j = 0; j < 7; j++) {
+                        const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
+                        if (__ballot(!(Tt < ej))) sm |= 1u << j;
+                        if (__ballot(!(Tt + ahead < ej))) lm |= 1u << j;
+                    }
+                    const int nl = __popcll(__ballot(event));
+                    const int nc = __popcll(__ballot(!(Tt < bs.E[4 * SR_E_STRIDE])));
+                    {
+                        const unsigned long long cb = __ballot(!(Tt < bs.E[4 * SR_E_STRIDE]));
+                        if (cb && (int)__lane_id() == __builtin_ctzll(cb))
+                            printf("[cy] i %d lane %d E4 %g H %g u %g du %g cm %x T %g par %x ro %g %g %g\n", i, (int)__lane_id(),
+                                   bs.E[4 * SR_E_STRIDE], bs.E[BS::L::SLAB0 * SR_E_STRIDE], r.u, r.du, bs.cm(), Tt, par,
+                                   Bp.x, Bp.y, Bp.z);
+                    }
+                    if (r.dbg)
+                        printf("[ev] i %d nl %d spent %x look %x ncyl %d T %g ahead %g E %g %g %g %g %g %g %g H %g u %g du %g cm %x\n",
+                               i, nl, sm, lm, nc, Tt, ahead, bs.E[0], bs.E[1 * SR_E_STRIDE], bs.E[2 * SR_E_STRIDE],
+                               bs.E[3 * SR_E_STRIDE], bs.E[4 * SR_E_STRIDE], bs.E[5 * SR_E_STRIDE], bs.E[6 * SR_E_STRIDE],
+                               bs.E[BS::L::SLAB0 * SR_E_STRIDE], r.u, r.du, bs.cm());
+                }
+#endif
                 // the inner window's bound for this lane: steep falling lanes get bh_u3
                 const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
                                      fr.u_f, fr.bh_u2, fr.bh_u3, steep);
                 if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
+#ifdef SR_DEBUG_PX
+                if (r.dbg)
+                    printf("[re] i %d reach %x E4 %g H %g m %g\n", i, reach, bs.E[4 * SR_E_STRIDE],
+                           bs.E[BS::L::SLAB0 * SR_E_STRIDE], bs.m());
+                if (__ballot(r.dbg)) {
+                    const unsigned long long cb = __ballot(bs.E[4 * SR_E_STRIDE] < 0.05f);
+                    if (cb && (int)__lane_id() == __builtin_ctzll(cb))
+                        printf("[cy2] i %d lane %d E4 %g H %g\n", i, (int)__lane_id(), bs.E[4 * SR_E_STRIDE],
+                               bs.E[BS::L::SLAB0 * SR_E_STRIDE]);
+                }
+#endif
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach & 0x1ffu; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
