@@ -185,7 +185,7 @@ def parse():
                     help="rows of the frame swept on the CPU for `value` (0 = every row: the full frame)")
     ap.add_argument("--single-frame", choices=["on", "off"], default="on",
                     help="also time single-frame launches (N = 1): one frame alone, and 4 in flight")
-    ap.add_argument("--single-split", default="32:16:1200",
+    ap.add_argument("--single-split", default="64:16:800",
                     help="split tiles for the latency figure of one frame alone: max_tiles[:lanes[:min_steps]] "
                          "(0 = off; the costliest tiles' rays in sparse waves, DESIGN.md §6)")
     ap.add_argument("--dump-frames", default="",

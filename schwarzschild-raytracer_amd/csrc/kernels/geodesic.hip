@@ -2084,6 +2084,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     const unsigned prof_bi_ = (unsigned)clock64();  // budget_init's cycles (section 22)
 #endif
     if (!CULL) bs.setUhi(INFINITY);
+#ifdef SR_INIT_TWICE  // timing experiments only: what budget_init costs (run it twice)
+    if (CULL) {
+        budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2);
+        asm volatile("" : "+v"(r.ro.x), "+v"(r.ro.y), "+v"(r.ro.z), "+v"(r.tv.x), "+v"(r.tv.y), "+v"(r.tv.z));
+    }
+#endif
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                     fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2);
