@@ -380,6 +380,9 @@ __device__ __forceinline__ void test_object(Hit& best, const sr_dev_obj& ob, int
 #ifndef SR_NEAR
 #define SR_NEAR 1.0f
 #endif
+#ifndef SR_CYL_INSIDE
+#define SR_CYL_INSIDE 1
+#endif
 #ifndef SR_XPLANE  // orbital-plane exclusion of bounded slots (budget_frame)
 #define SR_XPLANE 1
 #endif
@@ -418,7 +421,11 @@ __device__ __forceinline__ float clearance_obj(const sr_dev_slot& sl, f3 A, floa
                 } else if (sl.type == SR_OBJECT_HOLLOW_DISK) {
                     er = fmaxf(0.0f, fmaxf(sl.x0 - rho, rho - sl.x1));
                 } else {
-                    er = fmaxf(0.0f, rho - sl.x1);
+                    // the lateral surface alone (no caps): inside the tube
+                    // too, its distance is |rho - radius| (SR_CYL_INSIDE; a
+                    // solid cylinder's 0 made every step of a ray travelling
+                    // up the tube an event)
+                    er = SR_CYL_INSIDE ? fabsf(rho - sl.x1) : fmaxf(0.0f, rho - sl.x1);
                     ey = fmaxf(0.0f, fmaxf(-y, y - sl.x0));
                 }
                 d2 = er * er + ey * ey;
