@@ -553,6 +553,25 @@ def test_negative_u_exits(pkg, gpu, oracle, oracle_tex, max_steps, revs):
         assert (o[2] == max_steps).sum() > 50  # rays that ran to the end of the loop
 
 
+@pytest.mark.parametrize("max_steps,revs,closest", [(2000, 2, 10.0), (1000, 2, 4.0), (600, 2, 4.0), (300, 1, 6.0)])
+def test_black_hole_crossings(pkg, gpu, oracle, oracle_tex, max_steps, revs, closest):
+    """Rays falling into the hole (geodesic.hip SR_BH_WINDOW2 / SR_BH_CROSS):
+    the inner window down to the frame's bound and crossings that end as
+    ST_BH without an event. Step angles on both sides of SR_BH_S_DPHI (the
+    steep lanes' 6e-5 bound at 2000 and 1000 steps over two revolutions, the
+    1.5e-3 one at 600 and 300), flyby cameras 4-10 units from the hole so
+    that much of the frame falls in. Whole 320x180 frames, bit-exact with
+    step counts."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    cam = abi.camera_flyby(0.5, 30.0, closest)
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, max_revolutions=revs)
+    g = gpu_debug(gpu, scene, cam, params, 320, 180)
+    o = oracle.render(scene, cam, params, 320, 180, oracle_tex)
+    print(compare(g, o, f"{max_steps} steps, {revs} revolutions, closest {closest}"))
+    assert (o[2] < max_steps).sum() > 0
+
+
 def test_reference_assets_frame(pkg, oracle):
     """The reference's own textures through the ingest path (assets/textures:
     2k.jpg skybox, uv_checker.jpg + cubemap.png array, image_utils.cpp:7-117)
