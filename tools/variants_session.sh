@@ -1,7 +1,7 @@
 #!/bin/bash
 # Bench lines for the non-headline BASELINE.json configs and the SURVEY §8(f)
 # row-3 variants (split modes 2/3, noise mask 0.75, reference loop without
-# culling), and the headline with single-frame launches and a flyby camera. One bench.py process per line, each under its own time limit;
+# culling, the max-capacity scene and the press-R overlay at config 2's size), and the headline with single-frame launches and a flyby camera. One bench.py process per line, each under its own time limit;
 # a failure ends the session.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -27,5 +27,7 @@ run half_width 180 --mode half_width --steps 20 --warmup 3 || exit $?
 run half_height 180 --mode half_height --steps 20 --warmup 3 || exit $?
 run flat 180 --mode flat --steps 20 --warmup 3 || exit $?
 run noise075 180 --percent-black 0.75 --steps 20 --warmup 3 || exit $?
+run stress 240 --workload small --scene stress --steps 20 --warmup 3 || exit $?
+run testray 300 --workload small --test-ray on --single-frame off --steps 20 --warmup 3 || exit $?
 run no_cull 300 --no-cull --steps 3 --warmup 1 || exit $?
 echo "session done"
