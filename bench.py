@@ -185,9 +185,11 @@ def parse():
                     help="rows of the frame swept on the CPU for `value` (0 = every row: the full frame)")
     ap.add_argument("--single-frame", choices=["on", "off"], default="on",
                     help="also time single-frame launches (N = 1): one frame alone, and 4 in flight")
-    ap.add_argument("--single-split", default="64:16:800",
+    ap.add_argument("--single-split", default="0",
                     help="split tiles for the latency figure of one frame alone: max_tiles[:lanes[:min_steps]] "
-                         "(0 = off; the costliest tiles' rays in sparse waves, DESIGN.md §6)")
+                         "(0 = off, the default since the black hole's crossing change: every split setting "
+                         "measured 2-8 %% slower alone, profiles/r05/s32; the costliest tiles' rays in sparse "
+                         "waves, DESIGN.md §6)")
     ap.add_argument("--dump-frames", default="",
                     help="directory: rank 0 saves every timed frame as assembled (frame_<f>.npy), for the "
                          "multi-rank parity test; copies are taken after the timed region")
