@@ -234,7 +234,17 @@ typedef struct {
     // and out_dip / (1 + SR_BH_G3) for steep falling lanes (E >= SR_BH_E_MIN)
     // when max_dphi <= SR_BH_S_DPHI (else bh_u2); both rounded down
     float bh_u2, bh_u3;
+    // per budgeted cylinder k (sr_dev_slot.cyl): the orbital-plane distance of
+    // its bounding centre beyond which no chord of a low-energy orbit (u <
+    // 0.6, u'^2 + u^2 (1 - u) <= SR_XCYL_EMAX) can reach it (geodesic.hip
+    // SR_XCYL, sr_api.cpp xcyl_need); +inf: never excluded
+    float xcyl_need[SR_MAX_CYLINDERS];
 } sr_dev_frame;
+
+// the orbit energy below which a cylinder's orbital-plane exclusion applies
+// (under the photon orbit's 4/27: such an orbit outside the photon sphere
+// stays at u <= 0.58, so |u'| <= sqrt(E) and |u''| <= 1/6 along it)
+#define SR_XCYL_EMAX 0.14f
 
 // the inner black-hole window's margins (sr_api.cpp build_frame, geodesic.hip)
 #define SR_BH_G2 1.5e-3

@@ -94,9 +94,6 @@ struct Tex {
     const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
-#ifdef SR_STATS_NEARBH
-__device__ int sr_nearbh_prints;
-#endif
 // budget slots 0 .. 8 have their own counters in measurement builds
 #define SR_STATS_SLOTS 9
 #ifdef SR_STATS
@@ -802,6 +799,22 @@ __device__ __forceinline__ uint32_t xplane_bit(const sr_dev_slot& sl, int j, f3 
     // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
     return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
 }
+// A budgeted cylinder off a low-energy orbit's plane (SR_XCYL): need =
+// sr_dev_frame.xcyl_need (sr_api.cpp xcyl_need has the bound: the chords
+// that could come near the cylinder by distance from the origin stay short
+// enough that its quadratic margin is small). The slab budget (nearly
+// parallel chords) is left alone, as for outward lanes (outward_slot).
+#ifndef SR_XCYL
+#define SR_XCYL 1
+#endif
+__device__ __forceinline__ uint32_t xcyl_bit(const sr_dev_slot& sl, int j, f3 n, float nn, float need) {
+    const float h = dot(ld3(sl.bc), n);
+    return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
+}
+// the orbit's energy allows the exclusion (NaN: no)
+__device__ __forceinline__ bool xcyl_orbit(float u, float du) {
+    return u < 0.6f && __builtin_fmaf(du, du, u * u * (1.0f - u)) <= SR_XCYL_EMAX;
+}
 // the cylinders' (pa, pb) rows and the cm bits (budget_frame, budget_init)
 template <class BS>
 __device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
@@ -822,7 +835,8 @@ __device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restr
     return cm;
 }
 template <class BS>
-__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv, float xs) {
+__device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv, float xs,
+                                             const float* xneed, bool lowe) {
     const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
     uint32_t x = 0;
 #if SR_XPLANE
@@ -847,7 +861,11 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         const f3 n = cross(nv, tv);  // |n| within 1e-5 of 1
         const float nn = dot(n, n);
         const int nb = sc->num_budget;
-        for (int j = 1; j <= nb; j++) x |= xplane_bit(sc->slots[j - 1], j, n, nn, xs);
+        for (int j = 1; j <= nb; j++) {
+            x |= xplane_bit(sc->slots[j - 1], j, n, nn, xs);
+            if (SR_XCYL && sc->slots[j - 1].type == SR_OBJECT_CYLINDER && lowe)
+                x |= xcyl_bit(sc->slots[j - 1], j, n, nn, xneed[sc->slots[j - 1].cyl]);
+        }
     }
 #endif
     bs.setCm(cm, x);
@@ -863,7 +881,8 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 
 template <class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
-                                            bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w) {
+                                            bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w,
+                                            const float* xneed, bool lowe) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.setT(0.0f);
@@ -905,6 +924,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         const sr_dev_slot sl = pin_slot(nxt);
         if (j < nb) nxt = sc->slots[j];
         if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn, xs);
+        if (SR_XCYL && sl.type == SR_OBJECT_CYLINDER && lowe) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[sl.cyl]);
         float e = clearance_obj(sl, A, a) - m0;
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
@@ -1232,7 +1252,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
                                      ((bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u),
                              a, dip))
                 v = INFINITY;
-            if (TY != SR_OBJECT_PLANE && TY != SR_OBJECT_CYLINDER && ((xcl >> j) & 1u)) v = INFINITY;  // budget_frame
+            if (TY != SR_OBJECT_PLANE && ((xcl >> j) & 1u)) v = INFINITY;  // budget_frame (cylinders: SR_XCYL)
             bs.E[j * SR_E_STRIDE] = v;
             m = nmin(m, v);
             if (TY == SR_OBJECT_CYLINDER) {
@@ -1359,11 +1379,7 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                                  uint32_t reach, f3 o, f3 d, float seg) {
     Hit best = no_hit();
-#ifdef SR_NO_TR_CULL  // timing experiments only
-    test_ray_hits(sc, segs, best, o, d, seg);
-#else
     test_ray_hits_culled(sc, segs, best, o, d, seg);
-#endif
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
@@ -1845,14 +1861,8 @@ struct Ray {
     f3 ro, rd, nv, tv;
     float u, du;
     int i, steps;
-#ifdef SR_DEBUG_PX  // debugging builds only: printf trace of one pixel (x, y, kernel)
-    int dbg;
-#endif
 #ifdef SR_PROF
     unsigned* prof;  // the wave's 8 section accumulators in LDS
-#endif
-#ifdef SR_STATS_NEARBH
-    int px, py;
 #endif
 #ifdef SR_STATS
     int ev, mat;  // budget events, exact chords (measurement builds)
@@ -2091,16 +2101,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     const unsigned prof_bi_ = (unsigned)clock64();  // budget_init's cycles (section 22)
 #endif
     if (!CULL) bs.setUhi(INFINITY);
-#ifdef SR_INIT_TWICE  // timing experiments only: what budget_init costs (run it twice)
-    if (CULL) {
-        budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2);
-        asm volatile("" : "+v"(r.ro.x), "+v"(r.ro.y), "+v"(r.ro.z), "+v"(r.tv.x), "+v"(r.tv.y), "+v"(r.tv.z));
-    }
-#endif
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2);
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xcyl_need,
+                    xcyl_orbit(r.u, r.du));
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -2190,7 +2194,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
                 r.u = 1.0f / len(q);
                 r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s);
+                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s, fr.xcyl_need, xcyl_orbit(r.u, r.du));
                 force = true;  // the chord starts at the exact r.ro
             }
             SR_PT(1);
@@ -2417,11 +2421,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // to the origin, then inf / NaN): the exact chord is degenerate (zero
         // length, NaN direction) and the exact tests decide what its NaN
         // arithmetic hits, so every slot is tested (reach below)
-#ifdef SR_NO_DEGEN  // timing experiments only
-        const bool degen = false;
-#else
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
-#endif
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
 #ifndef SR_BH_CROSS
 #define SR_BH_CROSS 1
@@ -2432,11 +2432,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             const float uin = (uhi == fr.bh_u3 && fr.bh_u3 != fr.bh_u2) ? SR_BH_UIN3 : SR_BH_UIN2;
             if (BS::inner(uhi) && un >= uin && un < 1.0e30f && vb < 0.0f && !force) return ST_BH;
         }
-#ifdef SR_DEBUG_PX
-        if (r.dbg)
-            printf("[%d] slow i %d u %.9g un %.9g du %.9g vb %g bhx %d ev %d uhi %g E0 %g T %g m %g excl %x\n", r.dbg, i,
-                   r.u, un, r.du, vb, (int)bhx, (int)event, uhi, bs.E[0], bs.T(), bs.m(), bs.excl());
-#endif
         if (CULL) {  // the radii of the step's ends (the fast loop carries none)
             rA = __builtin_amdgcn_rcpf(r.u);
             rB = __builtin_amdgcn_rcpf(un);
@@ -2501,11 +2496,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                         SR_STAT(50 + bk, nl);
                     }
 #elif defined(SR_STATS_NEAR)
-#ifdef SR_STATS_NEARBH
-#define SR_STATS_NEARBH_ON 1
-#else
-#define SR_STATS_NEARBH_ON 0
-#endif
                     // measurement only (tools/stats_frame.py --near): back-to-back events
                     {
                         // slots some lane has spent at this event (bit j), by interval 1 (44..46:
@@ -2519,32 +2509,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                             if (__ballot(!(Tt < ej))) sm |= 1u << j;
                         }
                         const int ns = __popc(sm);
-#ifndef SR_STATS_NEARBH
                         SR_STAT((iv <= 1 ? 44 : 47) + (ns <= 1 ? 0 : ns == 2 ? 1 : 2), 1);
-#endif
                         if (iv <= 1) {
                             near_run++;
-#ifdef SR_STATS_NEARBH  // the lanes spending the black hole's slot alone at interval 1, by u and sign of u'
-                            if (sm == 1u) {
-                                const bool own = !(Tt < bs.E[0]);
-                                const float uu = r.u;
-                                const int ub = uu < 0.986f ? 0 : uu < 0.996f ? 1 : uu < 1.0f ? 2 : uu < 1.01f ? 3 : uu < 1.5f ? 4 : 5;
-                                for (int k = 0; k < 6; k++) {
-                                    SR_STAT(44 + k, __popcll(__ballot(own && ub == k && r.du > 0.0f)));
-                                    SR_STAT(50 + k, __popcll(__ballot(own && ub == k && !(r.du > 0.0f))));
-                                }
-                                // a few lanes in long runs: where they are
-                                if (near_run >= 8 && own && (int)__lane_id() == __builtin_ctzll(__ballot(own)) &&
-                                    atomicAdd(&sr_nearbh_prints, 1) < 24)
-                                    printf("nearbh px %d py %d i %d run %d u %.9g du %.9g up %.9g T %g E0 %g m %g uhi %g E %g\n",
-                                           r.px, r.py, i, near_run, r.u, r.du, up, Tt, bs.E[0], bs.m(), bs.uhi(),
-                                           r.du * r.du + r.u * r.u * (1.0f - r.u));
-                            }
-#else
                             if (ns == 1) SR_STAT(55 + __builtin_ctz(sm), 1);
-#endif
                         } else if (near_run > 0) {
-                            if (!SR_STATS_NEARBH_ON) SR_STAT(50 + (near_run <= 1 ? 0 : near_run <= 3 ? 1 : near_run <= 7 ? 2 : near_run <= 15 ? 3 : 4), 1);
+                            SR_STAT(50 + (near_run <= 1 ? 0 : near_run <= 3 ? 1 : near_run <= 7 ? 2 : near_run <= 15 ? 3 : 4), 1);
                             near_run = 0;
                         }
                     }
@@ -2561,6 +2531,30 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                             SR_STAT(44 + j, __popcll(__ballot(own && ring)));
                             SR_STAT(51 + j, __popcll(__ballot(own && !ring)));
                             if (j < 6 && __ballot(!(Tt + ahead < ej)) && !__ballot(own)) SR_STAT(58 + j, 1);
+                        }
+                    }
+#elif defined(SR_STATS_XCYL)  // measurement only (tools/stats_frame.py --xcyl): the cylinder's spends by plane distance
+                    if (sc->budget_cyl_mask) {
+                        // lanes spending the first budgeted cylinder (44), of them those whose orbital
+                        // plane is farther than br + d from its bounding centre, d = 0.25, 1, 2, 4
+                        // (45..48); events spending it (49), spending it alone (54), and alone with
+                        // only such lanes (50..53)
+                        const int jc = __builtin_ctz((uint32_t)sc->budget_cyl_mask) + 1;
+                        const sr_dev_slot& sl = sc->slots[jc - 1];
+                        const float Tt = bs.T();
+                        uint32_t sm = 0;
+                        for (int j = 0; j <= sc->num_budget; j++)
+                            if (__ballot(!(Tt < bs.E[j * SR_E_STRIDE]))) sm |= 1u << j;
+                        const bool own = !(Tt < bs.E[jc * SR_E_STRIDE]);
+                        const f3 n = cross(r.nv, r.tv);
+                        const float h = fabsf(dot(ld3(sl.bc), n)) * __builtin_amdgcn_rsqf(dot(n, n)) - sl.br;
+                        const float dd[4] = {0.25f, 1.0f, 2.0f, 4.0f};
+                        SR_STAT(44, __popcll(__ballot(own)));
+                        if (__ballot(own)) SR_STAT(49, 1);
+                        if (sm == (1u << jc)) SR_STAT(54, 1);
+                        for (int k = 0; k < 4; k++) {
+                            SR_STAT(45 + k, __popcll(__ballot(own && h > dd[k])));
+                            if (sm == (1u << jc) && !__ballot(own && !(h > dd[k]))) SR_STAT(50 + k, 1);
                         }
                     }
 #else
@@ -2630,48 +2624,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     SR_STAT(31, __popcll(__ballot(any)));
                 }
 #endif
-#ifdef SR_DEBUG_PX  // the debug lane's wave: what each event spends and looks ahead at
-                if (__ballot(r.dbg)) {
-                    uint32_t sm = 0, lm = 0;
-                    const float Tt = bs.T();
-                    for (int j = 0; j < 7; j++) {
-                        const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
-                        if (__ballot(!(Tt < ej))) sm |= 1u << j;
-                        if (__ballot(!(Tt + ahead < ej))) lm |= 1u << j;
-                    }
-                    const int nl = __popcll(__ballot(event));
-                    const int nc = __popcll(__ballot(!(Tt < bs.E[4 * SR_E_STRIDE])));
-                    {
-                        const unsigned long long cb = __ballot(!(Tt < bs.E[4 * SR_E_STRIDE]));
-                        if (cb && (int)__lane_id() == __builtin_ctzll(cb))
-                            printf("[cy] i %d lane %d E4 %g H %g u %g du %g cm %x T %g par %x ro %g %g %g\n", i, (int)__lane_id(),
-                                   bs.E[4 * SR_E_STRIDE], bs.E[BS::L::SLAB0 * SR_E_STRIDE], r.u, r.du, bs.cm(), Tt, par,
-                                   Bp.x, Bp.y, Bp.z);
-                    }
-                    if (r.dbg)
-                        printf("[ev] i %d nl %d spent %x look %x ncyl %d T %g ahead %g E %g %g %g %g %g %g %g H %g u %g du %g cm %x\n",
-                               i, nl, sm, lm, nc, Tt, ahead, bs.E[0], bs.E[1 * SR_E_STRIDE], bs.E[2 * SR_E_STRIDE],
-                               bs.E[3 * SR_E_STRIDE], bs.E[4 * SR_E_STRIDE], bs.E[5 * SR_E_STRIDE], bs.E[6 * SR_E_STRIDE],
-                               bs.E[BS::L::SLAB0 * SR_E_STRIDE], r.u, r.du, bs.cm());
-                }
-#endif
                 // the inner window's bound for this lane: steep falling lanes get bh_u3
                 const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
                                      fr.u_f, fr.bh_u2, fr.bh_u3, steep);
                 if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
-#ifdef SR_DEBUG_PX
-                if (r.dbg)
-                    printf("[re] i %d reach %x E4 %g H %g m %g\n", i, reach, bs.E[4 * SR_E_STRIDE],
-                           bs.E[BS::L::SLAB0 * SR_E_STRIDE], bs.m());
-                if (__ballot(r.dbg)) {
-                    const unsigned long long cb = __ballot(bs.E[4 * SR_E_STRIDE] < 0.05f);
-                    if (cb && (int)__lane_id() == __builtin_ctzll(cb))
-                        printf("[cy2] i %d lane %d E4 %g H %g\n", i, (int)__lane_id(), bs.E[4 * SR_E_STRIDE],
-                               bs.E[BS::L::SLAB0 * SR_E_STRIDE]);
-                }
-#endif
                 SR_PT(6);
 #ifdef SR_STATS
                 for (uint32_t c = reach & 0x1ffu; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
@@ -2694,11 +2652,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             float seg = len(delta);
             r.rd = delta / seg;
             hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
-#ifdef SR_DEBUG_PX
-            if (r.dbg)
-                printf("[%d] exact i %d reach %x hit slot %d dist %g |prev| %g |ro| %g\n", r.dbg, i, reach, hit.slot, hit.dist,
-                       len(prev), len(r.ro));
-#endif
             SR_PT(4);
             if (hit.slot != SLOT_NONE) {
                 const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
@@ -2876,14 +2829,6 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         Ray r;
         Hit hit;
         int st = init_pixel(fr, fr.cam[frame], q, r);
-#ifdef SR_STATS_NEARBH
-        r.px = q.px;
-        r.py = q.py;
-#endif
-#ifdef SR_DEBUG_PX
-        r.dbg = (q.px == SR_DEBUG_PX && q.py == SR_DEBUG_PY) ? 1 : 0;
-        if (r.dbg) printf("[1] init st %d u %.9g du %.9g\n", st, r.u, r.du);
-#endif
 #ifdef SR_LANE_MASK  // latency experiments only (tools/lane_mask.py): masked pixels run no ray
         if (sr_lane_mask && !sr_lane_mask[(size_t)q.py * fr.width + q.px]) st = ST_DONE;
 #endif
@@ -2892,9 +2837,6 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[23] += (unsigned)(clock64() - prof_t0);
 #endif
         if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
-#ifdef SR_DEBUG_PX
-        if (r.dbg) printf("[1] end st %d steps %d logged %d i %d\n", st, r.steps, log.n, r.i);
-#endif
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
 #if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
@@ -3143,10 +3085,6 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         r.du = ps.at(PS_DU, id);
         r.i = ps.geti(PS_I, id) + 1;
         r.steps = (int)((unsigned)__float_as_int(rec.x) >> 8);
-#ifdef SR_DEBUG_PX
-        r.dbg = (q.px == SR_DEBUG_PX && q.py == SR_DEBUG_PY) ? 2 : 0;
-        if (r.dbg) printf("[2] resume i %d steps %d u %.9g du %.9g\n", r.i, r.steps, r.u, r.du);
-#endif
         HitLog log{ps, 0};  // RECORD = false: nothing is logged
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();

@@ -56,6 +56,9 @@ struct sr_ctx {
     bool scene_set = false;
     bool cull = true;
     sr_dev_scene h_scene;
+    // xcyl_need's last inputs and results (build_frame; cleared by sr_set_scene)
+    float xc_uf = NAN, xc_dphi = NAN;
+    float xc_need[SR_MAX_CYLINDERS];
     // pixel pipeline scratch (geodesic.hip): SR_PS_FIELDS planes of ps_n floats,
     // the resume worklist and its counter; grown on demand, reused per frame.
     // Renders on one context are ordered on its stream(s) by the caller.
@@ -665,6 +668,51 @@ void build_cam(const sr_camera* cam, sr_dev_cam& dc) {
     dc.ray_forward = 1.0f / (float)std::tan((double)(cam->fov / 360.0f * kPi));
 }
 
+// The orbital-plane exclusion of a budgeted cylinder (geodesic.hip SR_XCYL)
+// for a low-energy orbit: u < 0.6 and E = u'^2 + u^2 (1 - u) <= SR_XCYL_EMAX
+// at its start. E is conserved along the orbit (u'' = -u + 1.5 u^2; RK4's
+// drift over a frame is orders below the 2 % allowed here), so u stays below
+// 0.58, |u'| <= sqrt(E) and |u''| <= 1/6, and one step changes u by at most
+// kappa = sqrt(E) dphi + dphi^2 / 12. A chord whose nearer end lies at r_lo
+// has its farther end within r_hi = 1 / (1 / r_lo - kappa) (and within 2 /
+// u_f unless it is forced, budget_event), so S = |o|_1 + len + 1 <= (sqrt 3
+// + 1) r_hi + r_lo + 1, and the chord stays r_lo cos(dphi) from the origin.
+// may_hit accepts it only within br + mu S + qk (S + |pos|_1)^2 of the
+// bounding centre (chords off the axis by SR_BUDGET_DPMIN; the nearly
+// parallel ones are the slab budget's). Chords with r_lo >= r_c, where
+// r_lo cos(dphi) - |bc| exceeds that reach, cannot hit; the others have S <=
+// S(r_c), so a bounding centre farther than reach(S(r_c)) from the orbital
+// plane cannot be reached by any chord of the orbit. r_c is found on a
+// geometric grid, each interval [r_i, r_i+1] checked with its worst ends.
+static float xcyl_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
+    if (!(u_f > 0.0f) || !(sl.x1 > 0.0f) || !(max_dphi > 0.0f)) return INFINITY;
+    const double d = (double)max_dphi * 1.001;
+    const double kap = std::sqrt((double)SR_XCYL_EMAX) * 1.02 * d + d * d / 12.0 * 1.02 + 1e-6;
+    const double R2 = 2.0 / (double)u_f * (1.0 + 1e-5);
+    const auto rhi = [&](double r) {
+        const double v = 1.0 / r - kap;
+        return v > 1.0 / R2 ? 1.0 / v : R2;
+    };
+    const auto S = [&](double r) { return (std::sqrt(3.0) + 1.0) * rhi(r) * (1.0 + 1e-5) + r + 1.0; };
+    const auto reach = [&](double s) {
+        const double sc = s + (double)sl.pl1;
+        return ((double)sl.br + (double)sl.mu * s + (double)sl.qk * sc * sc) * 1.001 + 1e-4;
+    };
+    const double c = (1.0 - d * d / 2.0) * (1.0 - 1e-4);
+    // from the top (R2) down while every interval clears by distance
+    double hi = R2, rc = R2;
+    for (;;) {
+        const double lo = std::max(1.0, hi / 1.002);
+        if (!(lo * c - (double)sl.cn - reach(S(hi)) > 0.0)) break;
+        rc = lo;
+        if (lo <= 1.0) break;
+        hi = lo;
+    }
+    if (rc >= R2) return INFINITY;
+    const double need = reach(S(rc)) + 1e-6 * rhi(rc);
+    return std::nextafter((float)need, INFINITY);
+}
+
 int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
     if (!cam || !p || width <= 0 || height <= 0) return SR_E_INVALID;
     if (p->raytrace_type < 0 || p->raytrace_type > 3) return SR_E_INVALID;
@@ -672,6 +720,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     // the hand-off packs a ray's step count into 24 bits (geodesic.hip ps_word)
     if (p->max_steps < 0 || p->max_steps > SR_MAX_STEPS) return SR_E_INVALID;
     std::memset(&fr, 0, sizeof fr);
+    for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = INFINITY;  // launch() sets them
     build_cam(cam, fr.cam[0]);
     fr.batch = 1;
     // frag:860 (launch invariant, same float ops)
@@ -742,6 +791,19 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.num_budget = ctx->h_scene.num_budget;
     fr.num_budget_cyl = __builtin_popcount((unsigned)ctx->h_scene.budget_cyl_mask);
     fr.win_ok = fr.uf_radius <= 100.0f;
+    {  // the cylinders' orbital-plane exclusions (xcyl_need), per (u_f, step angle)
+        if (!(ctx->xc_uf == fr.u_f && ctx->xc_dphi == fr.max_dphi)) {
+            for (int k = 0; k < SR_MAX_CYLINDERS; k++) ctx->xc_need[k] = INFINITY;
+            for (int j = 0; j < ctx->h_scene.num_budget; j++) {
+                const sr_dev_slot& sl = ctx->h_scene.slots[j];
+                if (sl.type == SR_OBJECT_CYLINDER && sl.cyl >= 0 && sl.cyl < SR_MAX_CYLINDERS)
+                    ctx->xc_need[sl.cyl] = xcyl_need(sl, fr.u_f, fr.max_dphi);
+            }
+            ctx->xc_uf = fr.u_f;
+            ctx->xc_dphi = fr.max_dphi;
+        }
+        for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = ctx->xc_need[k];
+    }
     for (int f = 0; f < n_frames; f++) {
         const float* q = fr.cam[f].pos;
         if (!((double)q[0] * q[0] + (double)q[1] * q[1] + (double)q[2] * q[2] <= 1.0e4)) fr.win_ok = 0;
@@ -1050,6 +1112,7 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
         !hip_ok(hipStreamSynchronize(c->upload)))
         return SR_E_HIP;
     c->h_scene = d;
+    c->xc_uf = c->xc_dphi = NAN;  // xcyl_need again at the next launch
     c->scene_set = true;
     return SR_OK;
 }

@@ -742,3 +742,28 @@ def test_objects_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f):
     g = gpu_debug(gpu, scene, cam, params, 160, 90)
     o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
     print(compare(g, o, f"objects near orbital planes, u_f {u_f}"))
+
+
+@pytest.mark.parametrize("u_f,max_steps,t,d", [
+    (0.01, 1200, 7.0, 2.9), (0.01, 600, 7.0, 4.0), (0.01, 1200, 4.0, 2.7),
+    (0.05, 1200, -8.0, 3.2), (1.0e-4, 1200, 7.0, 3.0)])
+def test_cylinder_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f, max_steps, t, d):
+    """The cylinder's orbital-plane exclusion for low-energy orbits
+    (geodesic.hip SR_XCYL, sr_api.cpp xcyl_need: about br + 0.3 at the
+    default step angle and u_f = 0.01, +inf at u_f = 1e-4). Every orbital
+    plane holds the line through the camera and the hole; the cylinder's
+    base sits at t along it and d off it, so its bounding centre is at 0 ..
+    d + 2 from the planes of the frame's rays, across the exclusion's
+    threshold. Two step angles (600 and 1200 steps, two revolutions), whole
+    160x90 frames, bit-exact with step counts."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    line = np.array([0.0, 2.0, 15.0]) / np.linalg.norm([0.0, 2.0, 15.0])
+    pos = line * t + np.array([d, 0.0, 0.0])
+    for k in range(3):
+        scene.cylinders[0].transform.pos[k] = float(np.float32(pos[k]))
+    cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f)
+    g = gpu_debug(gpu, scene, cam, params, 160, 90)
+    o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
+    print(compare(g, o, f"cylinder near orbital planes, u_f {u_f}, {max_steps} steps, t {t}, d {d}"))

@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--trig", action="store_true", help="an SR_STATS_TRIG build (counters 44..63)")
     ap.add_argument("--stephist", action="store_true", help="an SR_STATS_STEPHIST build (counters 44..55)")
     ap.add_argument("--near", action="store_true", help="an SR_STATS_NEAR build (counters 44..61)")
-    ap.add_argument("--nearbh", action="store_true", help="with --near: an SR_STATS_NEARBH build")
+    ap.add_argument("--xcyl", action="store_true", help="an SR_STATS_XCYL build (counters 44..54)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch  # noqa: F401  (HIP runtime up before the library)
@@ -97,11 +97,15 @@ def main():
             out["spent_slots_longer"] = dict(zip(["1", "2", "3+"], [int(hi[15 + k]) for k in range(3)]))
             out["interval1_runs"] = dict(zip(["1", "2-3", "4-7", "8-15", "16+"], [int(hi[18 + k]) for k in range(5)]))
             out["interval1_one_slot_by_slot"] = [int(hi[23 + j]) for j in range(7)]
-            if args.nearbh:  # SR_STATS_NEARBH: lanes spending the hole's slot alone, by u bin and u' sign
-                bins = ["<0.986", "0.986-0.996", "0.996-1", "1-1.01", "1.01-1.5", ">=1.5"]
-                out = {k: v for k, v in out.items() if not k.startswith(("spent_slots", "interval1_"))}
-                out["bh_alone_lanes_infalling"] = dict(zip(bins, [int(hi[12 + k]) for k in range(6)]))
-                out["bh_alone_lanes_other"] = dict(zip(bins, [int(hi[18 + k]) for k in range(6)]))
+        if args.xcyl:  # an SR_STATS_XCYL build: the first budgeted cylinder's spends by orbital-plane distance
+            for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
+                out.pop(k, None)
+            ds = ["0.25", "1", "2", "4"]
+            out["cyl_spent_lanes"] = int(hi[12])
+            out["cyl_spent_lanes_plane_beyond_br_plus"] = dict(zip(ds, [int(hi[13 + k]) for k in range(4)]))
+            out["cyl_events"] = int(hi[17])
+            out["cyl_alone_events"] = int(hi[22])
+            out["cyl_alone_events_all_lanes_beyond_br_plus"] = dict(zip(ds, [int(hi[18 + k]) for k in range(4)]))
         if args.trig:  # an SR_STATS_TRIG build: counters 44..63 hold the lanes that spent each slot
             for k in ("event_lanes", "events_bh_window_only", "interval1_small_budget_lanes_by_slot"):
                 out.pop(k, None)
