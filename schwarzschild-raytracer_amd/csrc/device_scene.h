@@ -239,6 +239,10 @@ typedef struct {
     // 0.6, u'^2 + u^2 (1 - u) <= SR_XCYL_EMAX) can reach it (geodesic.hip
     // SR_XCYL, sr_api.cpp xcyl_need); +inf: never excluded
     float xcyl_need[SR_MAX_CYLINDERS];
+    // per budget slot j - 1: the orbit energy at or below which a low-energy
+    // orbit's periapsis lies beyond every chord that could reach the object
+    // (geodesic.hip SR_XPERI, sr_api.cpp xperi_e); -1: never excluded
+    float xperi_e[SR_MAX_BUDGET];
 } sr_dev_frame;
 
 // the orbit energy below which a cylinder's orbital-plane exclusion applies

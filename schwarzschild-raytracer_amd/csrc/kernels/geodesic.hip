@@ -811,10 +811,20 @@ __device__ __forceinline__ uint32_t xcyl_bit(const sr_dev_slot& sl, int j, f3 n,
     const float h = dot(ld3(sl.bc), n);
     return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
 }
-// the orbit's energy allows the exclusion (NaN: no)
-__device__ __forceinline__ bool xcyl_orbit(float u, float du) {
-    return u < 0.6f && __builtin_fmaf(du, du, u * u * (1.0f - u)) <= SR_XCYL_EMAX;
+// The orbit's energy E = u'^2 + u^2 (1 - u) for the exclusions of low-energy
+// orbits (SR_XCYL, SR_XPERI: u < 0.6 and E <= SR_XCYL_EMAX), +inf otherwise
+// (NaN compares false too)
+__device__ __forceinline__ float orbit_e(float u, float du) {
+    return u < 0.6f ? __builtin_fmaf(du, du, u * u * (1.0f - u)) : INFINITY;
 }
+// Periapsis exclusion (SR_XPERI): a low-energy orbit never comes closer to
+// the origin than its periapsis, and an object whose every reachable chord
+// (sr_api.cpp clear_radius) lies inside that sphere is excluded for the
+// orbit, like an orbital-plane exclusion (bits 8 + j, budget_frame). The
+// accretion disk, within r = 5 of the hole, is the default scene's case.
+#ifndef SR_XPERI
+#define SR_XPERI 1
+#endif
 // the cylinders' (pa, pb) rows and the cm bits (budget_frame, budget_init)
 template <class BS>
 __device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv) {
@@ -836,7 +846,7 @@ __device__ __forceinline__ uint32_t budget_cyl_frame(const sr_dev_scene* __restr
 }
 template <class BS>
 __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc, BS& bs, f3 nv, f3 tv, float xs,
-                                             const float* xneed, bool lowe) {
+                                             const float* xneed, const float* xperi, float eo) {
     const uint32_t cm = budget_cyl_frame(sc, bs, nv, tv);
     uint32_t x = 0;
 #if SR_XPLANE
@@ -863,8 +873,9 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         const int nb = sc->num_budget;
         for (int j = 1; j <= nb; j++) {
             x |= xplane_bit(sc->slots[j - 1], j, n, nn, xs);
-            if (SR_XCYL && sc->slots[j - 1].type == SR_OBJECT_CYLINDER && lowe)
+            if (SR_XCYL && sc->slots[j - 1].type == SR_OBJECT_CYLINDER && eo <= SR_XCYL_EMAX)
                 x |= xcyl_bit(sc->slots[j - 1], j, n, nn, xneed[sc->slots[j - 1].cyl]);
+            if (SR_XPERI && eo <= xperi[j - 1]) x |= 1u << j;
         }
     }
 #endif
@@ -882,7 +893,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 template <class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w,
-                                            const float* xneed, bool lowe) {
+                                            const float* xneed, const float* xperi, float eo) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.setT(0.0f);
@@ -924,7 +935,8 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         const sr_dev_slot sl = pin_slot(nxt);
         if (j < nb) nxt = sc->slots[j];
         if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn, xs);
-        if (SR_XCYL && sl.type == SR_OBJECT_CYLINDER && lowe) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[sl.cyl]);
+        if (SR_XCYL && sl.type == SR_OBJECT_CYLINDER && eo <= SR_XCYL_EMAX) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[sl.cyl]);
+        if (SR_XPERI && eo <= xperi[j - 1]) xcl |= 1u << j;
         float e = clearance_obj(sl, A, a) - m0;
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
@@ -2104,7 +2116,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                     fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xcyl_need,
-                    xcyl_orbit(r.u, r.du));
+                    fr.xperi_e, orbit_e(r.u, r.du));
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {
@@ -2194,7 +2206,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
                 r.u = 1.0f / len(q);
                 r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s, fr.xcyl_need, xcyl_orbit(r.u, r.du));
+                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s, fr.xcyl_need, fr.xperi_e,
+                                          orbit_e(r.u, r.du));
                 force = true;  // the chord starts at the exact r.ro
             }
             SR_PT(1);

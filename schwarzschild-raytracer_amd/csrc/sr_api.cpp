@@ -59,6 +59,7 @@ struct sr_ctx {
     // xcyl_need's last inputs and results (build_frame; cleared by sr_set_scene)
     float xc_uf = NAN, xc_dphi = NAN;
     float xc_need[SR_MAX_CYLINDERS];
+    float xc_peri[SR_MAX_BUDGET];
     // pixel pipeline scratch (geodesic.hip): SR_PS_FIELDS planes of ps_n floats,
     // the resume worklist and its counter; grown on demand, reused per frame.
     // Renders on one context are ordered on its stream(s) by the caller.
@@ -684,8 +685,13 @@ void build_cam(const sr_camera* cam, sr_dev_cam& dc) {
 // S(r_c), so a bounding centre farther than reach(S(r_c)) from the orbital
 // plane cannot be reached by any chord of the orbit. r_c is found on a
 // geometric grid, each interval [r_i, r_i+1] checked with its worst ends.
-static float xcyl_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
-    if (!(u_f > 0.0f) || !(sl.x1 > 0.0f) || !(max_dphi > 0.0f)) return INFINITY;
+// Both return r_c with reach(S(r_c)) (clear_radius; r_c = +inf: none).
+struct ClearRadius {
+    double rc, need, rhi;
+};
+static ClearRadius clear_radius(const sr_dev_slot& sl, float u_f, float max_dphi) {
+    ClearRadius out{INFINITY, INFINITY, INFINITY};
+    if (!(u_f > 0.0f) || !(max_dphi > 0.0f) || !std::isfinite(sl.br) || !std::isfinite(sl.cn)) return out;
     const double d = (double)max_dphi * 1.001;
     const double kap = std::sqrt((double)SR_XCYL_EMAX) * 1.02 * d + d * d / 12.0 * 1.02 + 1e-6;
     const double R2 = 2.0 / (double)u_f * (1.0 + 1e-5);
@@ -708,9 +714,33 @@ static float xcyl_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
         if (lo <= 1.0) break;
         hi = lo;
     }
-    if (rc >= R2) return INFINITY;
-    const double need = reach(S(rc)) + 1e-6 * rhi(rc);
-    return std::nextafter((float)need, INFINITY);
+    if (rc >= R2) return out;
+    out.rc = rc;
+    out.need = reach(S(rc)) + 1e-6 * rhi(rc);
+    out.rhi = rhi(rc);
+    return out;
+}
+static float xcyl_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
+    if (sl.type != SR_OBJECT_CYLINDER || !(sl.x1 > 0.0f)) return INFINITY;
+    const ClearRadius c = clear_radius(sl, u_f, max_dphi);
+    return std::isfinite(c.need) ? std::nextafter((float)c.need, INFINITY) : INFINITY;
+}
+// The periapsis exclusion (geodesic.hip SR_XPERI): a low-energy orbit stays
+// at u <= u_t, the root of u^2 (1 - u) = E below 2/3 (f(u) = u^2 (1 - u)
+// increases there), so its chords' nearer ends lie at r >= 1 / u_t (end
+// points within 2e-5 of their radius). When that is beyond r_c (x 1.001), no
+// chord of the orbit can reach the object by distance from the origin alone:
+// E <= f(1 / (1.001 r_c)), less 0.1 % and 1e-6 for the energy's drift and
+// rounding, and at most SR_XCYL_EMAX (the step bound's premise). Planes and
+// the black hole are never excluded.
+static float xperi_e(const sr_dev_slot& sl, float u_f, float max_dphi) {
+    if (sl.type == SR_OBJECT_PLANE) return -1.0f;
+    const ClearRadius c = clear_radius(sl, u_f, max_dphi);
+    if (!std::isfinite(c.rc)) return -1.0f;
+    const double w = 1.0 / (c.rc * 1.001);
+    double e = w < 2.0 / 3.0 ? w * w * (1.0 - w) * (1.0 - 1e-3) - 1e-6 : (double)SR_XCYL_EMAX;
+    e = std::min(e, (double)SR_XCYL_EMAX);
+    return e > 0.0 ? std::nextafter((float)e, 0.0f) : -1.0f;
 }
 
 int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width, int height, sr_dev_frame& fr) {
@@ -721,6 +751,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     if (p->max_steps < 0 || p->max_steps > SR_MAX_STEPS) return SR_E_INVALID;
     std::memset(&fr, 0, sizeof fr);
     for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = INFINITY;  // launch() sets them
+    for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xperi_e[j] = -1.0f;
     build_cam(cam, fr.cam[0]);
     fr.batch = 1;
     // frag:860 (launch invariant, same float ops)
@@ -794,15 +825,18 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     {  // the cylinders' orbital-plane exclusions (xcyl_need), per (u_f, step angle)
         if (!(ctx->xc_uf == fr.u_f && ctx->xc_dphi == fr.max_dphi)) {
             for (int k = 0; k < SR_MAX_CYLINDERS; k++) ctx->xc_need[k] = INFINITY;
+            for (int j = 0; j < SR_MAX_BUDGET; j++) ctx->xc_peri[j] = -1.0f;
             for (int j = 0; j < ctx->h_scene.num_budget; j++) {
                 const sr_dev_slot& sl = ctx->h_scene.slots[j];
                 if (sl.type == SR_OBJECT_CYLINDER && sl.cyl >= 0 && sl.cyl < SR_MAX_CYLINDERS)
                     ctx->xc_need[sl.cyl] = xcyl_need(sl, fr.u_f, fr.max_dphi);
+                ctx->xc_peri[j] = xperi_e(sl, fr.u_f, fr.max_dphi);
             }
             ctx->xc_uf = fr.u_f;
             ctx->xc_dphi = fr.max_dphi;
         }
         for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = ctx->xc_need[k];
+        for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xperi_e[j] = ctx->xc_peri[j];
     }
     for (int f = 0; f < n_frames; f++) {
         const float* q = fr.cam[f].pos;

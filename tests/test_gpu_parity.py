@@ -767,3 +767,28 @@ def test_cylinder_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f, max_ste
     g = gpu_debug(gpu, scene, cam, params, 160, 90)
     o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
     print(compare(g, o, f"cylinder near orbital planes, u_f {u_f}, {max_steps} steps, t {t}, d {d}"))
+
+
+@pytest.mark.parametrize("u_f,max_steps,rs,rb", [
+    (0.01, 1200, 3.2, 4.0), (0.01, 600, 4.5, 5.5), (0.05, 1200, 2.6, 6.5), (1.0e-4, 1200, 3.2, 4.0)])
+def test_objects_near_periapsis(pkg, gpu, oracle, oracle_tex, u_f, max_steps, rs, rb):
+    """The periapsis exclusion (geodesic.hip SR_XPERI, sr_api.cpp xperi_e): a
+    low-energy orbit never comes closer to the hole than its periapsis, so
+    objects whose reachable chords all lie inside that sphere are excluded
+    for it. A sphere and a box moved close to the hole (centres at rs and rb
+    from it, beside the accretion disk within r = 5) put the exclusion's
+    threshold energy inside the frame's spread of impact parameters. Two step
+    angles and three u_f (1e-4: chords out to r = 2e4, the bound's large-r
+    clearing fails and nothing is excluded), whole 160x90 frames, bit-exact
+    with step counts."""
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    for k, v in enumerate((rs * 0.8, 0.0, rs * 0.6)):
+        scene.spheres[0].transform.pos[k] = v
+    for k, v in enumerate((-rb * 0.6, 0.5, -rb * 0.8)):
+        scene.boxes[0].transform.pos[k] = v
+    cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f)
+    g = gpu_debug(gpu, scene, cam, params, 160, 90)
+    o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
+    print(compare(g, o, f"objects near periapsis, u_f {u_f}, {max_steps} steps, sphere at {rs}, box at {rb}"))
