@@ -885,6 +885,25 @@ def scene_variant(args) -> str:
     return "stress" if args.scene == "stress" else ("testray" if args.test_ray == "on" else "default")
 
 
+def counter_variant(args) -> str:
+    """The key of a line's PMC / traffic records: the scene variant, plus any
+    option that changes the integrate kernel's work per frame (mode, noise
+    mask, no culling, a moving camera). Only the lines the roofline sessions
+    measure (default, stress, testray) find records; the others print
+    `frac` null instead of another workload's counters."""
+    v = scene_variant(args)
+    mods = []
+    if getattr(args, "mode", "curved") != "curved":
+        mods.append(args.mode)
+    if getattr(args, "percent_black", -1.0) >= 0.0:
+        mods.append("noise")
+    if getattr(args, "no_cull", False):
+        mods.append("nocull")
+    if getattr(args, "camera", "static") != "static":
+        mods.append(args.camera)
+    return "_".join([v] + mods) if mods else v
+
+
 def profile_record(path: str, kind: str, variant: str) -> Path:
     """--pmc-json / --traffic-json, or profiles/<kind>_latest[_<variant>].json."""
     if path:
@@ -926,7 +945,7 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
     renders B frames and F launches overlap, `overlap` = kernel_ms / (B x
     ms_per_step)): it is what the rocprofv3 --stats summary of this command
     reports."""
-    variant = scene_variant(args)
+    variant = counter_variant(args)
     pmc = load_matching(profile_record(args.pmc_json, "pmc", variant), W, H, N, world, variant)
     share = sigma_steps_mine / max(1, sigma_steps_frame)  # rank 0's share of the frame's steps
     executed = None

@@ -200,4 +200,13 @@ def test_counter_records_keyed_by_scene_variant(tmp_path):
     del rec["variant"]  # records from before the variant key: the default scene
     p.write_text(json.dumps(rec))
     assert bench.load_matching(p, 640, 360, 1000, 1) == rec
+    # options that change the kernel's work per frame never read the default's counters
+    base = dict(scene="default", test_ray="off", mode="curved", percent_black=-1.0, no_cull=False, camera="static")
+    assert bench.counter_variant(argparse.Namespace(**base)) == "default"
+    for k, v, key in (("mode", "half_width", "default_half_width"), ("percent_black", 0.75, "default_noise"),
+                      ("no_cull", True, "default_nocull"), ("camera", "flyby", "default_flyby")):
+        key_got = bench.counter_variant(argparse.Namespace(**{**base, k: v}))
+        assert key_got == key
+        assert bench.load_matching(p, 640, 360, 1000, 1, key_got) is None
+    assert bench.counter_variant(argparse.Namespace(**{**base, "scene": "stress"})) == "stress"
     assert bench.load_matching(p, 640, 360, 1000, 1, "stress") is None
