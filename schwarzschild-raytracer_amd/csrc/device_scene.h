@@ -234,11 +234,11 @@ typedef struct {
     // and out_dip / (1 + SR_BH_G3) for steep falling lanes (E >= SR_BH_E_MIN)
     // when max_dphi <= SR_BH_S_DPHI (else bh_u2); both rounded down
     float bh_u2, bh_u3;
-    // per budgeted cylinder k (sr_dev_slot.cyl): the orbital-plane distance of
-    // its bounding centre beyond which no chord of a low-energy orbit (u <
-    // 0.6, u'^2 + u^2 (1 - u) <= SR_XCYL_EMAX) can reach it (geodesic.hip
-    // SR_XCYL, sr_api.cpp xcyl_need); +inf: never excluded
-    float xcyl_need[SR_MAX_CYLINDERS];
+    // per budget slot j - 1: the orbital-plane distance of its bounding centre
+    // beyond which no chord of a low-energy orbit (u < 0.6, u'^2 + u^2 (1 -
+    // u) <= SR_XCYL_EMAX) can reach it (geodesic.hip SR_XCYL, sr_api.cpp
+    // xlow_need); +inf: never excluded
+    float xlow_need[SR_MAX_BUDGET];
     // per budget slot j - 1: the orbit energy at or below which a low-energy
     // orbit's periapsis lies beyond every chord that could reach the object
     // (geodesic.hip SR_XPERI, sr_api.cpp xperi_e); -1: never excluded

@@ -799,11 +799,13 @@ __device__ __forceinline__ uint32_t xplane_bit(const sr_dev_slot& sl, int j, f3 
     // |h| / sqrt(nn) > need without a square root; NaN frames exclude nothing
     return (uint32_t)(h * h > (need * need) * (nn * 1.0002f)) << j;
 }
-// A budgeted cylinder off a low-energy orbit's plane (SR_XCYL): need =
-// sr_dev_frame.xcyl_need (sr_api.cpp xcyl_need has the bound: the chords
-// that could come near the cylinder by distance from the origin stay short
-// enough that its quadratic margin is small). The slab budget (nearly
-// parallel chords) is left alone, as for outward lanes (outward_slot).
+// A bounded slot off a low-energy orbit's plane (SR_XCYL): need =
+// sr_dev_frame.xlow_need[j - 1] (sr_api.cpp xlow_need has the bound: the
+// chords that could come near the object by distance from the origin stay
+// short, so its margin mu S, and a cylinder's quadratic one, are small; the
+// orbital-plane exclusion's S_max gave a cylinder 31 units). A cylinder's
+// slab budget (nearly parallel chords) is left alone, as for outward lanes
+// (outward_slot).
 #ifndef SR_XCYL
 #define SR_XCYL 1
 #endif
@@ -873,8 +875,7 @@ __device__ __forceinline__ void budget_frame(const sr_dev_scene* __restrict__ sc
         const int nb = sc->num_budget;
         for (int j = 1; j <= nb; j++) {
             x |= xplane_bit(sc->slots[j - 1], j, n, nn, xs);
-            if (SR_XCYL && sc->slots[j - 1].type == SR_OBJECT_CYLINDER && eo <= SR_XCYL_EMAX)
-                x |= xcyl_bit(sc->slots[j - 1], j, n, nn, xneed[sc->slots[j - 1].cyl]);
+            if (SR_XCYL && eo <= SR_XCYL_EMAX) x |= xcyl_bit(sc->slots[j - 1], j, n, nn, xneed[j - 1]);
             if (SR_XPERI && eo <= xperi[j - 1]) x |= 1u << j;
         }
     }
@@ -935,7 +936,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         const sr_dev_slot sl = pin_slot(nxt);
         if (j < nb) nxt = sc->slots[j];
         if (SR_XPLANE) xcl |= xplane_bit(sl, j, xn, xnn, xs);
-        if (SR_XCYL && sl.type == SR_OBJECT_CYLINDER && eo <= SR_XCYL_EMAX) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[sl.cyl]);
+        if (SR_XCYL && eo <= SR_XCYL_EMAX) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[j - 1]);
         if (SR_XPERI && eo <= xperi[j - 1]) xcl |= 1u << j;
         float e = clearance_obj(sl, A, a) - m0;
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
@@ -2115,7 +2116,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xcyl_need,
+                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xlow_need,
                     fr.xperi_e, orbit_e(r.u, r.du));
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
@@ -2206,7 +2207,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 r.tv = nrm(cross(cross(r.nv, r.rd), r.nv));
                 r.u = 1.0f / len(q);
                 r.du = -r.u * dot(r.rd, r.nv) / dot(r.rd, r.tv);
-                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s, fr.xcyl_need, fr.xperi_e,
+                if (CULL) budget_frame(sc, bs, r.nv, r.tv, fr.xplane_s, fr.xlow_need, fr.xperi_e,
                                           orbit_e(r.u, r.du));
                 force = true;  // the chord starts at the exact r.ro
             }

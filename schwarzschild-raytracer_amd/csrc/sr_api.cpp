@@ -56,9 +56,9 @@ struct sr_ctx {
     bool scene_set = false;
     bool cull = true;
     sr_dev_scene h_scene;
-    // xcyl_need's last inputs and results (build_frame; cleared by sr_set_scene)
+    // xlow_need's and xperi_e's last inputs and results (build_frame; cleared by sr_set_scene)
     float xc_uf = NAN, xc_dphi = NAN;
-    float xc_need[SR_MAX_CYLINDERS];
+    float xc_need[SR_MAX_BUDGET];
     float xc_peri[SR_MAX_BUDGET];
     // pixel pipeline scratch (geodesic.hip): SR_PS_FIELDS planes of ps_n floats,
     // the resume worklist and its counter; grown on demand, reused per frame.
@@ -720,10 +720,13 @@ static ClearRadius clear_radius(const sr_dev_slot& sl, float u_f, float max_dphi
     out.rhi = rhi(rc);
     return out;
 }
-static float xcyl_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
-    if (sl.type != SR_OBJECT_CYLINDER || !(sl.x1 > 0.0f)) return INFINITY;
+// (every bounded slot: for spheres mu S(r_c) replaces the orbital-plane
+// exclusion's mu S_max, 0.96 for the quadratic factor; for a cylinder it is
+// the only plane exclusion; + 1e-5 |bc| for the plane distance's rounding)
+static float xlow_need(const sr_dev_slot& sl, float u_f, float max_dphi) {
+    if (sl.type == SR_OBJECT_PLANE || (sl.type == SR_OBJECT_CYLINDER && !(sl.x1 > 0.0f))) return INFINITY;
     const ClearRadius c = clear_radius(sl, u_f, max_dphi);
-    return std::isfinite(c.need) ? std::nextafter((float)c.need, INFINITY) : INFINITY;
+    return std::isfinite(c.need) ? std::nextafter((float)(c.need + 1e-5 * (double)sl.cn), INFINITY) : INFINITY;
 }
 // The periapsis exclusion (geodesic.hip SR_XPERI): a low-energy orbit stays
 // at u <= u_t, the root of u^2 (1 - u) = E below 2/3 (f(u) = u^2 (1 - u)
@@ -750,7 +753,7 @@ int build_frame(sr_ctx* ctx, const sr_camera* cam, const sr_params* p, int width
     // the hand-off packs a ray's step count into 24 bits (geodesic.hip ps_word)
     if (p->max_steps < 0 || p->max_steps > SR_MAX_STEPS) return SR_E_INVALID;
     std::memset(&fr, 0, sizeof fr);
-    for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = INFINITY;  // launch() sets them
+    for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xlow_need[j] = INFINITY;  // launch() sets them
     for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xperi_e[j] = -1.0f;
     build_cam(cam, fr.cam[0]);
     fr.batch = 1;
@@ -822,20 +825,19 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     fr.num_budget = ctx->h_scene.num_budget;
     fr.num_budget_cyl = __builtin_popcount((unsigned)ctx->h_scene.budget_cyl_mask);
     fr.win_ok = fr.uf_radius <= 100.0f;
-    {  // the cylinders' orbital-plane exclusions (xcyl_need), per (u_f, step angle)
+    {  // the low-energy exclusions (xlow_need, xperi_e), per (u_f, step angle)
         if (!(ctx->xc_uf == fr.u_f && ctx->xc_dphi == fr.max_dphi)) {
-            for (int k = 0; k < SR_MAX_CYLINDERS; k++) ctx->xc_need[k] = INFINITY;
+            for (int j = 0; j < SR_MAX_BUDGET; j++) ctx->xc_need[j] = INFINITY;
             for (int j = 0; j < SR_MAX_BUDGET; j++) ctx->xc_peri[j] = -1.0f;
             for (int j = 0; j < ctx->h_scene.num_budget; j++) {
                 const sr_dev_slot& sl = ctx->h_scene.slots[j];
-                if (sl.type == SR_OBJECT_CYLINDER && sl.cyl >= 0 && sl.cyl < SR_MAX_CYLINDERS)
-                    ctx->xc_need[sl.cyl] = xcyl_need(sl, fr.u_f, fr.max_dphi);
+                ctx->xc_need[j] = xlow_need(sl, fr.u_f, fr.max_dphi);
                 ctx->xc_peri[j] = xperi_e(sl, fr.u_f, fr.max_dphi);
             }
             ctx->xc_uf = fr.u_f;
             ctx->xc_dphi = fr.max_dphi;
         }
-        for (int k = 0; k < SR_MAX_CYLINDERS; k++) fr.xcyl_need[k] = ctx->xc_need[k];
+        for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xlow_need[j] = ctx->xc_need[j];
         for (int j = 0; j < SR_MAX_BUDGET; j++) fr.xperi_e[j] = ctx->xc_peri[j];
     }
     for (int f = 0; f < n_frames; f++) {
@@ -1146,7 +1148,7 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
         !hip_ok(hipStreamSynchronize(c->upload)))
         return SR_E_HIP;
     c->h_scene = d;
-    c->xc_uf = c->xc_dphi = NAN;  // xcyl_need again at the next launch
+    c->xc_uf = c->xc_dphi = NAN;  // xlow_need, xperi_e again at the next launch
     c->scene_set = true;
     return SR_OK;
 }
