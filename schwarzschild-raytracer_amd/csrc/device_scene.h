@@ -94,7 +94,7 @@ typedef struct {
     float bc[3], x0;
     float pos[3], x1;
     float a0[3], x2;  // axes[0..2] (columns)
-    float a1[3], pad0;
+    float a1[3], rf;  // rf: the farthest the object's accepted points reach from the origin (outward_slot)
     float a2[3], cn;  // cn: |bc| x 1.001, rounded up (outward_clear)
 } sr_dev_slot;  // 128 B
 

@@ -525,9 +525,18 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
 #ifndef SR_OUT_CYL_CM
 #define SR_OUT_CYL_CM 1
 #endif
+// Round 5: an outward lane clears an object once it is beyond the object's
+// farthest accepted point (sr_dev_slot.rf) rather than its bounding sphere's
+// far side: a disk seen edge-on from the origin, a rectangle or a cylinder's
+// rim lie well inside |bc| + br.
+#ifndef SR_OUT_FAR
+#define SR_OUT_FAR 1
+#endif
 __device__ __forceinline__ bool outward_slot(const sr_dev_slot& sl, bool cyl_par, float a, float dip) {
     if (SR_OUT_CYL_CM) cyl_par = false;
     if (sl.type == SR_OBJECT_PLANE || (sl.type == SR_OBJECT_CYLINDER && (cyl_par || !(sl.x1 > 0.0f)))) return false;
+    if (SR_OUT_FAR)  // the object's own farthest point (sr_api.cpp far_reach), not its bounding sphere's
+        return outward_clear(sl.rf, 0.0f, slot_mu(sl), sl.type == SR_OBJECT_CYLINDER ? sl.qk : 0.0f, sl.pl1, a, dip);
     return outward_clear(sl.cn, sl.br, sl.mu, sl.type == SR_OBJECT_CYLINDER ? sl.qk : 0.0f, sl.pl1, a, dip);
 }
 

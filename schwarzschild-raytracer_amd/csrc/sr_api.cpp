@@ -1050,6 +1050,63 @@ int sr_set_texture_array(sr_ctx* c, const uint8_t* px, int w, int h, int layers,
 }
 
 // The compact copy of a budgeted object (device_scene.h sr_dev_slot).
+// The farthest any point the object's exact test accepts can lie from the
+// origin (geodesic.hip outward_slot): the primitive's farthest point F plus
+// the larger of its static margins (the bounding sphere's and the
+// distance-to-primitive one, mp), x 1.001, rounded up; the per-chord terms
+// (mu S, a cylinder's quadratic margin) are outward_clear's. A disk's or a
+// rim's farthest point is sqrt((c . n)^2 + (|c_perp| + R)^2), a rectangle's
+// a corner, a sphere's |c| + R. At most cn + br (the bounding sphere's),
+// which boxes, planes and frames without a unit normal keep.
+static float far_reach(const sr_dev_obj& o, float cn) {
+    const double sphere = (double)cn + (double)o.br;
+    if (!(o.mp < INFINITY) || !std::isfinite(sphere)) return (float)sphere;
+    const float* f = o.f;
+    const double p[3] = {f[SR_F_POS], f[SR_F_POS + 1], f[SR_F_POS + 2]};
+    double a0[3], a1[3], a2[3];
+    for (int i = 0; i < 3; i++) {
+        a0[i] = f[SR_F_AXES + i];
+        a1[i] = f[SR_F_AXES + 3 + i];
+        a2[i] = f[SR_F_AXES + 6 + i];
+    }
+    const auto norm = [](const double* v) { return std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); };
+    const auto rim = [&](const double* c, double R) {  // circle centre c, normal a1, radius R
+        const double cn1 = c[0] * a1[0] + c[1] * a1[1] + c[2] * a1[2];
+        const double cp = std::sqrt(std::max(0.0, c[0] * c[0] + c[1] * c[1] + c[2] * c[2] - cn1 * cn1));
+        return std::sqrt(cn1 * cn1 + (cp + R) * (cp + R));
+    };
+    double F;
+    switch (o.type) {
+    case SR_OBJECT_DISK: F = rim(p, std::fabs((double)f[17])); break;
+    case SR_OBJECT_HOLLOW_DISK: F = rim(p, std::fabs((double)f[18])); break;
+    case SR_OBJECT_CYLINDER: {
+        const double h = f[SR_F_P0], R = std::fabs((double)f[SR_F_P0 + 1]);
+        const double top[3] = {p[0] + a1[0] * h, p[1] + a1[1] * h, p[2] + a1[2] * h};
+        F = std::max(rim(p, R), rim(top, R));
+        break;
+    }
+    case SR_OBJECT_RECTANGLE: {
+        const double w = f[17], h = f[18];
+        F = 0.0;
+        for (int i = 0; i < 4; i++) {
+            const double al = (i & 1) ? w : 0.0, be = (i & 2) ? h : 0.0;
+            const double c[3] = {p[0] + a0[0] * al + a2[0] * be, p[1] + a0[1] * al + a2[1] * be,
+                                 p[2] + a0[2] * al + a2[2] * be};
+            F = std::max(F, norm(c));
+        }
+        break;
+    }
+    default:
+        return (float)sphere;
+    }
+    // the bounding sphere's static margin mu (1 + |c|_1 + R) with R <= br, or mp
+    const double l1c = std::fabs((double)o.bc[0]) + std::fabs((double)o.bc[1]) + std::fabs((double)o.bc[2]);
+    const double margin = std::max((double)o.mu * (1.0 + l1c + (double)o.br), (double)o.mp);
+    const double rf = (F + margin) * 1.001;
+    if (!std::isfinite(rf) || !(rf < sphere)) return (float)sphere;
+    return std::nextafter((float)rf, INFINITY);
+}
+
 static void pack_slot(const sr_dev_obj& o, int cyl, sr_dev_slot& sl) {
     std::memset(&sl, 0, sizeof sl);
     const float* f = o.f;
@@ -1068,6 +1125,7 @@ static void pack_slot(const sr_dev_obj& o, int cyl, sr_dev_slot& sl) {
     std::memcpy(sl.a0, f + SR_F_AXES, 3 * sizeof(float));
     std::memcpy(sl.a1, f + SR_F_AXES + 3, 3 * sizeof(float));
     std::memcpy(sl.a2, f + SR_F_AXES + 6, 3 * sizeof(float));
+    sl.rf = far_reach(o, sl.cn);
     switch (o.type) {
     case SR_OBJECT_RECTANGLE:
     case SR_OBJECT_HOLLOW_DISK:
