@@ -546,6 +546,11 @@ def main():
         first, batch = last[0]
         parity = frame_parity(args, W, H, N, quality, use_assets, batch[-1], first + batch.shape[0] - 1)
     ktimes = np.concatenate([c[0].kernel_times(per_ctx) for c in ctxs], axis=0)
+    # frames of each row of ktimes: launch j of the window ran on context j % F
+    # (run_frames), and each context lists its own launches in order
+    sizes = [min(B, args.steps - f) for f in range(0, args.steps, B)]
+    launch_frames = np.array([sizes[j] for k in range(len(ctxs)) for j in range(k, len(sizes), F)], dtype=np.int64)
+    assert launch_frames.size == ktimes.shape[0], (launch_frames.size, ktimes.shape)
     if args.dump_frames and rank == 0:
         Path(args.dump_frames).mkdir(parents=True, exist_ok=True)
         for f, fr in frames.items():
@@ -553,7 +558,6 @@ def main():
         frames.clear()
     for c in ctxs:
         c[0].set_timing(0)
-    integrate_ms, shade_ms, resume_ms = (float(x) for x in ktimes.mean(axis=0))
 
     # frame latency (untimed for `value`): one launch of B frames alone on
     # context 0; every frame of it is done when the launch is
@@ -662,7 +666,7 @@ def main():
                     "frac_of_frame_latency": round(band_ms / latency_ms, 3)}
 
     if rank == 0:
-        roofline = make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_ms, resume_ms,
+        roofline = make_roofline(args, W, H, N, world, F, B, ms_per_step, ktimes, launch_frames,
                                  latency_ms, sigma_steps_frame, sigma_steps_mine, len(rows_mine), critical,
                                  speedup_ref)
         cpu = None
@@ -929,7 +933,34 @@ def load_matching(path, W, H, N, world, variant="default"):
     return rec
 
 
-def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_ms, resume_ms, latency_ms,
+def launch_accounting(ktimes, launch_frames, ms_per_step):
+    """Kernel time of the timed window's launches, which need not be equal
+    (20 frames in launches of 16 are [16, 4]): per integrate launch
+    (`kernel_ms`, the plain mean rocprofv3 --stats reports), per launch size,
+    per frame (total duration / frames), and `overlap` = total integrate
+    duration / the window (frames x ms_per_step): the mean number of
+    integrate launches in flight. ktimes: [launches, 3] ms (integrate, shade,
+    resume); launch_frames: frames of each launch."""
+    import numpy as np
+
+    kt = np.asarray(ktimes, dtype=np.float64).reshape(-1, 3)
+    lf = np.asarray(launch_frames, dtype=np.int64).reshape(-1)
+    assert kt.shape[0] == lf.size and lf.size > 0
+    window_ms = float(lf.sum()) * ms_per_step
+    by_size = {str(int(b)): round(float(kt[lf == b, 0].mean()), 4) for b in sorted(set(lf.tolist()), reverse=True)}
+    return {
+        "kernel_ms": round(float(kt[:, 0].mean()), 4),
+        "kernel_ms_by_launch_frames": by_size,
+        "kernel_ms_per_frame": round(float(kt[:, 0].sum() / lf.sum()), 4),
+        "launch_frames": lf.tolist(),
+        "overlap": round(float(kt[:, 0].sum()) / window_ms, 3),
+        "pipeline_ms_per_frame": {"integrate": round(float(kt[:, 0].sum() / lf.sum()), 4),
+                                  "shade": round(float(kt[:, 1].sum() / lf.sum()), 4),
+                                  "resume": round(float(kt[:, 2].sum() / lf.sum()), 4)},
+    }
+
+
+def make_roofline(args, W, H, N, world, F, B, ms_per_step, ktimes, launch_frames, latency_ms,
                   sigma_steps_frame, sigma_steps_mine, rows_mine, critical, speedup_ref):
     """Roofline of the dominant kernel (sr_integrate_kernel: ray generation,
     the step loop and every intersection test), on rank 0's launches.
@@ -941,10 +972,10 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
     --pmc on this kernel source and config, calibrated by
     tools/microbench/flops_calib.hip: profiles/pmc_latest.json) times the
     frames per second of this run, so `frac` is utilisation of the FP32 peak. `kernel_ms` is the same run's mean
-    integrate-launch duration (HIP events on each launch's stream; a launch
-    renders B frames and F launches overlap, `overlap` = kernel_ms / (B x
-    ms_per_step)): it is what the rocprofv3 --stats summary of this command
-    reports."""
+    integrate-launch duration (HIP events on each launch's stream): it is
+    what the rocprofv3 --stats summary of this command reports; launches of
+    unequal size are also reported per size and per frame, and `overlap` is
+    the total integrate duration over the timed window (launch_accounting)."""
     variant = counter_variant(args)
     pmc = load_matching(profile_record(args.pmc_json, "pmc", variant), W, H, N, world, variant)
     share = sigma_steps_mine / max(1, sigma_steps_frame)  # rank 0's share of the frame's steps
@@ -975,12 +1006,9 @@ def make_roofline(args, W, H, N, world, F, B, ms_per_step, integrate_ms, shade_m
         "traffic": traffic,
         "executed_flop_per_frame": None if executed is None else round(executed),
         "valu_issue_frac": None if valu_issue is None else round(valu_issue, 4),
-        "kernel_ms": round(integrate_ms, 4),
-        "overlap": round(integrate_ms / (B * ms_per_step), 2),
+        **launch_accounting(ktimes, launch_frames, ms_per_step),
         "launches_in_flight": F,
         "frames_per_launch": B,
-        "pipeline_ms": {"integrate": round(integrate_ms, 4), "shade": round(shade_ms, 4),
-                        "resume": round(resume_ms, 4)},
         # this rank's executed ray-steps of one frame (the debug render of the
         # first camera), and of one launch of B frames (static camera: B times
         # that; a flyby's frames differ, so none)

@@ -25,6 +25,8 @@ MAX_RECTANGLES = 3
 MAX_BOXES = 3
 MAX_OBJECTS = 21
 MAX_POINTS = 1000
+# floats per pixel of the integrate -> shade hand-off (csrc/device_scene.h SR_PS_FIELDS)
+PS_FIELDS = 4 + 8 * 4 + 16
 
 OBJECT_SPHERE, OBJECT_PLANE, OBJECT_DISK, OBJECT_HOLLOW_DISK = 0, 1, 2, 3
 OBJECT_CYLINDER, OBJECT_RECTANGLE, OBJECT_BOX = 4, 5, 6
@@ -208,6 +210,7 @@ EXTRA_SIGNATURES = {
     "sr_debug_set_timing": (_i, [_p, _i]),
     "sr_debug_kernel_times": (_i, [_p, C.POINTER(C.c_float), _i, C.POINTER(_i)]),
     "sr_debug_last_order": (_i, [_p, C.POINTER(_i), _i, C.POINTER(_i)]),
+    "sr_debug_pixel_state": (_i, [_p, C.POINTER(C.c_float), C.c_size_t, C.POINTER(C.c_size_t)]),
 }
 
 _lib = None

@@ -249,6 +249,13 @@ typedef struct {
 // (under the photon orbit's 4/27: such an orbit outside the photon sphere
 // stays at u <= 0.58, so |u'| <= sqrt(E) and |u''| <= 1/6 along it)
 #define SR_XCYL_EMAX 0.14f
+// the largest step angle (max_angle / max_steps, here max_dphi) at which the
+// low-energy exclusions apply (sr_api.cpp clear_radius): their premises (E
+// conserved within 2 %, one step moving u by at most kappa, u never past the
+// periapsis root) are checked on the kernel's own binary32 RK4 up to it by
+// tests/test_low_energy_bounds.py (the app's MAX_STEPS 100 at up to three
+// revolutions: 0.1885); coarser schedules exclude nothing
+#define SR_XLOW_DPHI_MAX 0.2f
 
 // the inner black-hole window's margins (sr_api.cpp build_frame, geodesic.hip)
 #define SR_BH_G2 1.5e-3

@@ -692,6 +692,7 @@ struct ClearRadius {
 static ClearRadius clear_radius(const sr_dev_slot& sl, float u_f, float max_dphi) {
     ClearRadius out{INFINITY, INFINITY, INFINITY};
     if (!(u_f > 0.0f) || !(max_dphi > 0.0f) || !std::isfinite(sl.br) || !std::isfinite(sl.cn)) return out;
+    if (!(max_dphi <= SR_XLOW_DPHI_MAX)) return out;  // the premises are proven up to this step angle
     const double d = (double)max_dphi * 1.001;
     const double kap = std::sqrt((double)SR_XCYL_EMAX) * 1.02 * d + d * d / 12.0 * 1.02 + 1e-6;
     const double R2 = 2.0 / (double)u_f * (1.0 + 1e-5);
@@ -1365,6 +1366,24 @@ int sr_debug_last_order(sr_ctx* c, int* out, int max_n, int* n) {
     const size_t k = c->last_slots < (size_t)max_n ? c->last_slots : (size_t)max_n;
     if (k && (!hip_ok(hipMemcpyAsync(out, c->last_order, k * sizeof(int), hipMemcpyDeviceToHost, c->upload)) ||
               !hip_ok(hipStreamSynchronize(c->upload))))
+        return SR_E_HIP;
+    return SR_OK;
+}
+
+// Not in sr.h's public set: a host copy of the integrate -> shade hand-off
+// (geodesic.hip PS_*: SR_PS_FIELDS floats per pixel id in its planes) after
+// the context's last frame, for post-mortems of single pixels without
+// instrumenting the kernel. *n_px = pixel ids the buffer holds; copies
+// min(max_floats, n_px * SR_PS_FIELDS) floats.
+int sr_debug_pixel_state(sr_ctx* c, float* out, size_t max_floats, size_t* n_px) {
+    if (!c || !n_px || (max_floats && !out)) return SR_E_INVALID;
+    *n_px = c->ps_n;
+    if (!max_floats || !c->d_ps) return SR_OK;
+    if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
+    size_t k = c->ps_n * SR_PS_FIELDS;
+    if (k > max_floats) k = max_floats;
+    if (!hip_ok(hipMemcpyAsync(out, c->d_ps, k * sizeof(float), hipMemcpyDeviceToHost, c->upload)) ||
+        !hip_ok(hipStreamSynchronize(c->upload)))
         return SR_E_HIP;
     return SR_OK;
 }

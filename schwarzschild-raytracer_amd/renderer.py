@@ -84,6 +84,16 @@ class Renderer:
         abi.check(self.lib.sr_debug_last_order(self.ctx, buf, n.value, C.byref(n)), "sr_debug_last_order")
         return np.frombuffer(buf, dtype=np.int32, count=n.value).copy()
 
+    def pixel_state(self) -> np.ndarray:
+        """The integrate -> shade hand-off after the last frame (post-mortems):
+        float32 [SR_PS_FIELDS * n] in geodesic.hip's PS layout, n pixel ids."""
+        n = C.c_size_t()
+        abi.check(self.lib.sr_debug_pixel_state(self.ctx, None, 0, C.byref(n)), "sr_debug_pixel_state")
+        buf = np.empty(max(1, n.value * abi.PS_FIELDS), dtype=np.float32)
+        abi.check(self.lib.sr_debug_pixel_state(self.ctx, buf.ctypes.data_as(C.POINTER(C.c_float)),
+                                                n.value * abi.PS_FIELDS, C.byref(n)), "sr_debug_pixel_state")
+        return buf[:n.value * abi.PS_FIELDS]
+
     def _stream(self, stream):
         if stream is None:
             stream = self.torch.cuda.current_stream(self.tdev)

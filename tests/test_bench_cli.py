@@ -170,12 +170,35 @@ def test_roofline_steps_per_frame_and_launch():
     frame_steps = launch_steps // B
     args = argparse.Namespace(pmc_json="/nonexistent", traffic_json="/nonexistent", camera="static",
                               scene="default", test_ray="off")
-    rf = bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None, None)
+    rf = bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, [[0.1, 0.01, 0.0]], [B], 0.3, frame_steps, frame_steps, H,
+                             None, None)
     assert rf["steps_per_frame"] == frame_steps and rf["frames_per_launch"] == B
     assert rf["steps_per_frame"] * rf["frames_per_launch"] == rf["steps_per_launch"] == launch_steps
     args.camera = "flyby"
-    assert bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, 0.1, 0.01, 0.0, 0.3, frame_steps, frame_steps, H, None,
-                               None)["steps_per_launch"] is None
+    assert bench.make_roofline(args, W, H, N, 1, 2, B, 0.1, [[0.1, 0.01, 0.0]], [B], 0.3, frame_steps, frame_steps,
+                               H, None, None)["steps_per_launch"] is None
+
+
+def test_launch_accounting_unequal_launches():
+    """The driver's 20-frame window in launches of 16 is [16, 4] (two
+    launches in flight): kernel_ms is the plain mean of the two durations (as
+    rocprofv3 --stats averages them), each size is reported apart, and
+    overlap is the total integrate duration over the window (VERDICT r5 #6)."""
+    import bench
+
+    ms_per_step = 0.8
+    kt = [[11.9, 0.9, 0.02], [3.6, 0.25, 0.01]]  # 16 frames, 4 frames (integrate, shade, resume)
+    acc = bench.launch_accounting(kt, [16, 4], ms_per_step)
+    assert acc["kernel_ms"] == round((11.9 + 3.6) / 2, 4)
+    assert acc["kernel_ms_by_launch_frames"] == {"16": 11.9, "4": 3.6}
+    assert acc["kernel_ms_per_frame"] == round((11.9 + 3.6) / 20, 4)
+    assert acc["overlap"] == round((11.9 + 3.6) / (20 * ms_per_step), 3)
+    assert acc["launch_frames"] == [16, 4]
+    assert acc["pipeline_ms_per_frame"]["shade"] == round(1.15 / 20, 4)
+    # the window's launches as bench.main orders ktimes: context k's launches j = k, k + F, ...
+    sizes = [min(16, 20 - f) for f in range(0, 20, 16)]
+    F = 2
+    assert [sizes[j] for k in range(F) for j in range(k, len(sizes), F)] == [16, 4]
 
 
 def test_counter_records_keyed_by_scene_variant(tmp_path):

@@ -744,18 +744,23 @@ def test_objects_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f):
     print(compare(g, o, f"objects near orbital planes, u_f {u_f}"))
 
 
-@pytest.mark.parametrize("u_f,max_steps,t,d", [
-    (0.01, 1200, 7.0, 2.9), (0.01, 600, 7.0, 4.0), (0.01, 1200, 4.0, 2.7),
-    (0.05, 1200, -8.0, 3.2), (1.0e-4, 1200, 7.0, 3.0)])
-def test_cylinder_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f, max_steps, t, d):
+@pytest.mark.parametrize("u_f,max_steps,t,d,revs", [
+    (0.01, 1200, 7.0, 2.9, 2), (0.01, 600, 7.0, 4.0, 2), (0.01, 1200, 4.0, 2.7, 2),
+    (0.05, 1200, -8.0, 3.2, 2), (1.0e-4, 1200, 7.0, 3.0, 2),
+    (0.01, 100, 7.0, 2.9, 2), (0.01, 100, 7.0, 3.4, 3), (0.01, 8000, 7.0, 2.9, 2), (0.01, 300, 4.0, 2.7, 1)])
+def test_cylinder_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f, max_steps, t, d, revs):
     """The cylinder's orbital-plane exclusion for low-energy orbits
     (geodesic.hip SR_XCYL, sr_api.cpp xcyl_need: about br + 0.3 at the
     default step angle and u_f = 0.01, +inf at u_f = 1e-4). Every orbital
     plane holds the line through the camera and the hole; the cylinder's
     base sits at t along it and d off it, so its bounding centre is at 0 ..
     d + 2 from the planes of the frame's rays, across the exclusion's
-    threshold. Two step angles (600 and 1200 steps, two revolutions), whole
-    160x90 frames, bit-exact with step counts."""
+    threshold. Step angles over the range the exclusions are enabled for
+    (sr_api.cpp clear_radius, SR_XLOW_DPHI_MAX; tests/test_low_energy_bounds.py
+    proves the premises there): the app's MAX_STEPS 100 (src/main.cpp:68) at
+    two and three revolutions (0.126, 0.188 rad), 300 steps at one, 600 and
+    1200 at two, and config 5's 8000; whole 160x90 frames, bit-exact with
+    step counts."""
     sc, abi = pkg.scenes, pkg.abi
     scene = sc.scene_default(textured=True)
     line = np.array([0.0, 2.0, 15.0]) / np.linalg.norm([0.0, 2.0, 15.0])
@@ -763,24 +768,27 @@ def test_cylinder_near_orbital_planes(pkg, gpu, oracle, oracle_tex, u_f, max_ste
     for k in range(3):
         scene.cylinders[0].transform.pos[k] = float(np.float32(pos[k]))
     cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
-    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f)
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f, max_revolutions=revs)
     g = gpu_debug(gpu, scene, cam, params, 160, 90)
     o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
-    print(compare(g, o, f"cylinder near orbital planes, u_f {u_f}, {max_steps} steps, t {t}, d {d}"))
+    print(compare(g, o, f"cylinder near orbital planes, u_f {u_f}, {max_steps} steps x {revs} revs, t {t}, d {d}"))
 
 
-@pytest.mark.parametrize("u_f,max_steps,rs,rb", [
-    (0.01, 1200, 3.2, 4.0), (0.01, 600, 4.5, 5.5), (0.05, 1200, 2.6, 6.5), (1.0e-4, 1200, 3.2, 4.0)])
-def test_objects_near_periapsis(pkg, gpu, oracle, oracle_tex, u_f, max_steps, rs, rb):
+@pytest.mark.parametrize("u_f,max_steps,rs,rb,revs", [
+    (0.01, 1200, 3.2, 4.0, 2), (0.01, 600, 4.5, 5.5, 2), (0.05, 1200, 2.6, 6.5, 2), (1.0e-4, 1200, 3.2, 4.0, 2),
+    (0.01, 100, 3.2, 4.0, 2), (0.01, 100, 4.5, 5.5, 3), (0.01, 8000, 3.2, 4.0, 2), (0.01, 300, 2.6, 6.5, 1)])
+def test_objects_near_periapsis(pkg, gpu, oracle, oracle_tex, u_f, max_steps, rs, rb, revs):
     """The periapsis exclusion (geodesic.hip SR_XPERI, sr_api.cpp xperi_e): a
     low-energy orbit never comes closer to the hole than its periapsis, so
     objects whose reachable chords all lie inside that sphere are excluded
     for it. A sphere and a box moved close to the hole (centres at rs and rb
     from it, beside the accretion disk within r = 5) put the exclusion's
-    threshold energy inside the frame's spread of impact parameters. Two step
-    angles and three u_f (1e-4: chords out to r = 2e4, the bound's large-r
-    clearing fails and nothing is excluded), whole 160x90 frames, bit-exact
-    with step counts."""
+    threshold energy inside the frame's spread of impact parameters. Step
+    angles over the range the exclusion is enabled for (100 steps at two and
+    three revolutions, 300 at one, 600 / 1200 at two, 8000; see
+    test_cylinder_near_orbital_planes) and three u_f (1e-4: chords out to r =
+    2e4, the bound's large-r clearing fails and nothing is excluded), whole
+    160x90 frames, bit-exact with step counts."""
     sc, abi = pkg.scenes, pkg.abi
     scene = sc.scene_default(textured=True)
     for k, v in enumerate((rs * 0.8, 0.0, rs * 0.6)):
@@ -788,7 +796,7 @@ def test_objects_near_periapsis(pkg, gpu, oracle, oracle_tex, u_f, max_steps, rs
     for k, v in enumerate((-rb * 0.6, 0.5, -rb * 0.8)):
         scene.boxes[0].transform.pos[k] = v
     cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
-    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f)
+    params = abi.default_params(max_steps=max_steps, percent_black=-1.0, u_f=u_f, max_revolutions=revs)
     g = gpu_debug(gpu, scene, cam, params, 160, 90)
     o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
-    print(compare(g, o, f"objects near periapsis, u_f {u_f}, {max_steps} steps, sphere at {rs}, box at {rb}"))
+    print(compare(g, o, f"objects near periapsis, u_f {u_f}, {max_steps} steps x {revs} revs, sphere at {rs}, box at {rb}"))
