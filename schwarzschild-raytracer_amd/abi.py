@@ -236,6 +236,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         raise FileNotFoundError(f"{p} not built; run __graft_entry__.build() or make -C schwarzschild-raytracer_amd")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
     for name, (res, args) in {**SIGNATURES, **EXTRA_SIGNATURES}.items():
+        if name in EXTRA_SIGNATURES and not hasattr(lib, name):
+            continue  # debug tooling an older library (a bisection build) may lack
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -2685,7 +2685,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 // r.steps: the ray's step count if this hit ends it
                 // the whole 32-byte sector in two 16-byte stores (a partial
                 // sector costs a read-modify-write)
-                float4* h = reinterpret_cast<float4*>(log.ps.hit32(log.id(), log.n));
+                // log.n < SR_PS_HITS by construction (ST_MORE below); the clamp
+                // keeps the store inside the hit planes whatever a miscompiled
+                // register holds (a 7-wave build of round
+                // 5's source counted 7 .. 31 hits and wrote past the planes)
+                float4* h = reinterpret_cast<float4*>(
+                    log.ps.hit32(log.id(), min((uint32_t)log.n, (uint32_t)(SR_PS_HITS - 1))));
                 h[0] = make_float4(hit.p.x, hit.p.y, hit.p.z,
                                    __int_as_float((int)((uint32_t)(hit.slot * 8 + hit.face + PS_KEY_BIAS) |
                                                                   ((uint32_t)r.steps << 8))));
@@ -3031,7 +3036,7 @@ __global__ __launch_bounds__(256, SR_SHADE_WAVES_PER_EU) void sr_shade_kernel(co
     tx.opq = nullptr;
     const float4 rec = ps.get_rec(id);
     const int w0 = __float_as_int(rec.x);
-    const int st = w0 & 7, nh = (w0 >> 3) & 7;
+    const int st = w0 & 7, nh = min((w0 >> 3) & 7, SR_PS_HITS);  // <= SR_PS_HITS written (memory safety)
     f4 frag = crosshair_frag(fr, q);
     bool done = false;
     int steps_at = -1;

@@ -16,11 +16,13 @@ from . import abi
 class Renderer:
     """One sr_ctx bound to one HIP device (the reference's single GL program)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, lib=None):
+        """lib: a loaded library (abi.load(path)) other than the package's
+        libsr.so, e.g. the test-only 7-wave build (tests/test_gpu_allocation.py)."""
         import torch
 
         self.torch = torch
-        self.lib = abi.load()
+        self.lib = lib if lib is not None else abi.load()
         self.device = int(device)
         self.tdev = torch.device("cuda", self.device)
         ctx = C.c_void_p()

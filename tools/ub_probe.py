@@ -51,6 +51,10 @@ def main():
     f, b, s = r.render_debug(abi.default_camera(), params, W, H)
     torch.cuda.synchronize()
     b, s = b.cpu().numpy(), s.cpu().numpy()
+    if not hasattr(r.lib, "sr_debug_pixel_state"):  # an older library (bisection): the frame only
+        np.save(out.replace(".json", "_frame.npy"), np.concatenate([b.astype(np.int32), s[..., None]], -1))
+        json.dump({"lib": os.environ.get("SR_LIB", "libsr.so")}, open(out, "w"))
+        return
     ps = r.pixel_state()
     n = ps.size // abi.PS_FIELDS
     res = {"lib": os.environ.get("SR_LIB", "libsr.so"), "n_ids": int(n), "pixels": []}
