@@ -2737,8 +2737,8 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 
 }  // namespace
 
-#ifndef SR_MIN_WAVES_PER_EU
-#define SR_MIN_WAVES_PER_EU 6
+#ifndef SR_MIN_WAVES_PER_EU  // the Makefile's WAVES (7 since round 6)
+#define SR_MIN_WAVES_PER_EU 7
 #endif
 #ifndef SR_NB_SMALL
 #define SR_NB_SMALL 6
@@ -2759,9 +2759,10 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #define SR_NC_GENERAL SR_MAX_CYLINDERS
 #define SR_LARGE_WAVES_PER_EU 4
 
-// Waves per SIMD the integrate kernel is built for: SR_MIN_WAVES_PER_EU (6:
-// 80 VGPRs) for the frame kernels of scenes that fit the small
-// instantiation; 5 (96 VGPRs) for the general one (8 slots, 3 cylinders),
+// Waves per SIMD the integrate kernel is built for: SR_MIN_WAVES_PER_EU (7:
+// 72 VGPRs, since round 6: 1.5 % more frames per second and one frame alone
+// 1.9 % sooner than 6 waves at 80, profiles/r06/s5) for the frame kernels of
+// scenes that fit the small instantiation; 5 (96 VGPRs) for the general one (8 slots, 3 cylinders),
 // whose event path then keeps every value in registers (at 6 it spilled 9 in
 // the reseed path), its 6.5 KiB of LDS per wave allowing 24 waves per CU
 constexpr int sr_integrate_waves(int nb, int nc) {

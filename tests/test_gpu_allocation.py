@@ -7,10 +7,12 @@ The post-mortem (tools/ub_probe.py over the
 integrate -> shade hand-off) found lanes of the overlay waves whose hit-log
 count, ray origin and direction were garbage (7 .. 31 logged hits, rd = -inf):
 registers corrupted, not a wrong decision. The present source is held to the
-same bits at two register allocations: `make` also builds
-lib/libsr_w7.so, the identical kernel source with the small instantiation at
-7 waves per SIMD, and every case here must equal the oracle's fixtures or
-libsr.so's own output bit for bit (float FragColor, RGBA8, step counts).
+same bits at two register allocations: libsr.so builds the small
+instantiation for 7 waves per SIMD since round 6 (72 VGPRs), and `make` also
+builds lib/libsr_alt.so, the identical kernel source at 6 waves per SIMD (80
+VGPRs; the Makefile's ALT_WAVES). Every case here must equal the oracle's
+fixtures or libsr.so's own output bit for bit (float FragColor, RGBA8, step
+counts).
 """
 from pathlib import Path
 
@@ -20,17 +22,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = Path(__file__).resolve().parent.parent
-LIB7 = ROOT / "schwarzschild-raytracer_amd" / "lib" / "libsr_w7.so"
+LIBALT = ROOT / "schwarzschild-raytracer_amd" / "lib" / "libsr_alt.so"
 BLOCK_ROWS = 8
 
 
 @pytest.fixture(scope="module")
-def lib7(pkg):
+def libalt(pkg):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    assert LIB7.exists(), "lib/libsr_w7.so not built (make -C schwarzschild-raytracer_amd)"
-    return pkg.abi.load(LIB7)
+    assert LIBALT.exists(), "lib/libsr_alt.so not built (make -C schwarzschild-raytracer_amd)"
+    return pkg.abi.load(LIBALT)
 
 
 @pytest.fixture(scope="module")
@@ -60,30 +62,31 @@ def debug(r, scene, cam, params, w, h, test_ray):
     return f.cpu().numpy().view(np.uint32), b.cpu().numpy(), s.cpu().numpy()
 
 
-def test_w7_library_is_the_7_wave_build(pkg, lib7):
+def test_alt_library_shares_the_abi(pkg, libalt):
     """The test library differs from libsr.so only in the kernel's
-    allocation: same ABI (struct sizes) and exports."""
+    allocation: same ABI (struct sizes)."""
     import ctypes as C
 
     n = 6
     a, b = (C.c_size_t * n)(), (C.c_size_t * n)()
     pkg.abi.load().sr_abi_struct_sizes(a, n)
-    lib7.sr_abi_struct_sizes(b, n)
+    libalt.sr_abi_struct_sizes(b, n)
     assert list(a) == list(b)
 
 
 @pytest.mark.parametrize("cfg,variant", [("c2t", "testray"), ("c2s", "stress"), ("c2", "default")])
-def test_w7_frames_exact(pkg, lib7, fh, assets, cfg, variant):
+def test_alt_frames_exact(pkg, libalt, fh, assets, cfg, variant):
     """The frames that failed in round 5's 7-wave build (c2t: the overlay's
     1000 cylinders, whose waves lost their registers), the max-capacity scene
-    and config 2: the debug render and two batched launches of four frames,
-    every row against the oracle's hashes (tests/golden/frame_hashes.npz)."""
+    and config 2, through the other allocation: the debug render and two
+    batched launches of four frames, every row against the oracle's hashes
+    (tests/golden/frame_hashes.npz)."""
     import torch
     from test_gpu_frames import frame_digest, sha_rows
 
     W, H, N = (int(v) for v in fh[f"{cfg}/config"])
     abi, sc = pkg.abi, pkg.scenes
-    r = pkg.Renderer(0, lib=lib7)
+    r = pkg.Renderer(0, lib=libalt)
     r.set_background(assets["2k"])
     r.set_texture_array(assets["arr"])
     scene = sc.scene_stress() if variant == "stress" else sc.scene_default(textured=True)
@@ -93,7 +96,7 @@ def test_w7_frames_exact(pkg, lib7, fh, assets, cfg, variant):
     _, b, s = debug(r, scene, cam, params, W, H, tr)
     rows = fh[f"{cfg}/rows"]
     bad = np.flatnonzero((sha_rows(b[rows]) != fh[f"{cfg}/rgba_sha"]).any(-1))
-    assert not len(bad), f"{cfg} (7-wave build): {len(bad)} RGBA8 rows differ, first {rows[bad[:5]].tolist()}"
+    assert not len(bad), f"{cfg} (the other allocation): {len(bad)} RGBA8 rows differ, first {rows[bad[:5]].tolist()}"
     assert not (sha_rows(s[rows].astype("<i4")) != fh[f"{cfg}/steps_sha"]).any(), f"{cfg}: step rows differ"
     B = 4
     for _ in range(2):
@@ -105,7 +108,7 @@ def test_w7_frames_exact(pkg, lib7, fh, assets, cfg, variant):
     r.close()
 
 
-def test_w7_golden_cases_equal_the_6_wave_build(pkg, lib7, golden, golden_cases, textures):
+def test_alt_golden_cases_equal_the_shipping_build(pkg, libalt, golden, golden_cases, textures):
     """Every golden case (the case set that faulted in round 5's 7-wave
     build) rendered by both allocations: identical float FragColor, RGBA8 and
     step counts (libsr.so is held to the oracle by test_golden_cases_bit_exact)."""
@@ -117,7 +120,7 @@ def test_w7_golden_cases_equal_the_6_wave_build(pkg, lib7, golden, golden_cases,
         by_kind.setdefault(case_texture_kind(golden, name), []).append(name)
     for kind, names in by_kind.items():
         arr = texture_array_of(pkg, kind)
-        rs = [pkg.Renderer(0), pkg.Renderer(0, lib=lib7)]
+        rs = [pkg.Renderer(0), pkg.Renderer(0, lib=libalt)]
         for r in rs:
             r.set_background(bg)
             r.set_texture_array(arr)
@@ -131,14 +134,14 @@ def test_w7_golden_cases_equal_the_6_wave_build(pkg, lib7, golden, golden_cases,
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_w7_random_scenes_and_overlays_equal(pkg, lib7, textures, seed):
+def test_alt_random_scenes_and_overlays_equal(pkg, libalt, textures, seed):
     """Random stress scenes (18-21 objects: the general and large
     instantiations, logged translucent hits, resumed rays) and random
     cameras with and without a visible test ray: both allocations agree
     bit for bit."""
     sc, abi = pkg.scenes, pkg.abi
     bg, arr = textures
-    rs = [pkg.Renderer(0), pkg.Renderer(0, lib=lib7)]
+    rs = [pkg.Renderer(0), pkg.Renderer(0, lib=libalt)]
     for r in rs:
         r.set_background(bg)
         r.set_texture_array(arr)
