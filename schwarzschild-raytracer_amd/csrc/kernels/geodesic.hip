@@ -513,6 +513,36 @@ __device__ __forceinline__ float plane_window(const sr_dev_slot& sl, f3 A, f3 B,
     const float f = 1.0f - (th1 * th1 + th1 * th0 + th0 * th0) * (1.0f / 6.0f);
     return (Lc > 0.0f && f > 0.0f) ? Lc * f * 0.998f : 0.0f;
 }
+// The same window from a ray's start (budget_init): the anchor A is the
+// camera (or a reseed point), where the orbit's tangent is the ray direction
+// d itself (the frame nv, tv and u' = -u (d . nv) / (d . tv) are built from
+// it: the tangent (nv cos phi + tv sin phi) / u differentiated at phi = 0 is
+// parallel to d, to rounding), so theta0 is that rounding's 1e-4 and no chord
+// enters it. Before it, every ray of a frame started with the distance budget
+// of the same camera point, and the rectangle in front of the default camera
+// (3.6 away) ran out on every wave at the same step: one event per wave.
+#ifndef SR_INIT_WINDOW
+#define SR_INIT_WINDOW 1
+#endif
+__device__ __forceinline__ float plane_window_start(const sr_dev_slot& sl, f3 A, f3 d, float a, float perr, float dphi) {
+    const f3 nrm_ = ld3(sl.a1);
+    const float y = dot(A - ld3(sl.pos), nrm_);
+    if (!(a > 1.0f)) return 0.0f;
+    const float a2 = a * a;
+    const float kap = 6.06f * __builtin_amdgcn_rcpf(a2);  // 6 / a^2 plus 1 %
+    const float c = (y > 0.0f ? -1.0f : 1.0f) * dot(d, nrm_);
+    const float th0 = 1e-4f;
+    const float m = (sl.mp + sl.mu * __builtin_fmaf(3.1f, a, 1.0f)) * 1.001f + perr;  // S <= 3.1 a + 1 (planar)
+    const float R = fabsf(y) - m;
+    if (!(R > 0.0f)) return 0.0f;
+    const float b = c + th0;
+    const float L = (__builtin_amdgcn_sqrtf(__builtin_fmaf(b, b, 2.0f * kap * R)) - b) * (a2 * (1.0f / 6.06f));
+    const float ch = 1.5f * a * dphi;  // the next chord
+    const float Lc = fminf(L, fminf(__builtin_fmaf(0.5f, a, -ch), (1.5f - th0) * (a2 * (1.0f / 6.06f)) - ch));
+    const float th1 = __builtin_fmaf(kap, Lc, th0);
+    const float f = 1.0f - (th1 * th1 + th1 * th0 + th0 * th0) * (1.0f / 6.0f);
+    return (Lc > 0.0f && f > 0.0f) ? Lc * f * 0.998f : 0.0f;
+}
 // slot j >= 1 for an outward lane at distance a (cyl_par: bs.cm's bit for a budgeted cylinder)
 // Round 5: a cylinder is excluded for outward lanes whose orbital plane can
 // hold a chord nearly parallel to its axis (bs.cm) too. Its distance budget
@@ -903,7 +933,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 template <class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w,
-                                            const float* xneed, const float* xperi, float eo) {
+                                            const float* xneed, const float* xperi, float eo, f3 d, float dphi) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
     const int nb = sc->num_budget;
     bs.setT(0.0f);
@@ -948,6 +978,12 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         if (SR_XCYL && eo <= SR_XCYL_EMAX) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[j - 1]);
         if (SR_XPERI && eo <= xperi[j - 1]) xcl |= 1u << j;
         float e = clearance_obj(sl, A, a) - m0;
+        if (SR_INIT_WINDOW && (sl.type == SR_OBJECT_RECTANGLE || sl.type == SR_OBJECT_DISK ||
+                               sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_PLANE) &&
+            sl.mp < INFINITY && e < 0.5f * a) {
+            const float w = plane_window_start(sl, A, d, a, m0, dphi);
+            e = w > e ? w : e;  // NaN e stays NaN
+        }
         if (outward && outward_slot(sl, cyl_par_bit(sc, bs, j), a, dip)) e = INFINITY;
         if ((xcl >> j) & 1u) e = INFINITY;  // off this orbit's plane (budget_frame)
         bs.E[j * SR_E_STRIDE] = e;
@@ -2126,7 +2162,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                     fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xlow_need,
-                    fr.xperi_e, orbit_e(r.u, r.du));
+                    fr.xperi_e, orbit_e(r.u, r.du),
+                    // the ray's start (sr_integrate_kernel): r.rd is the orbit's tangent at r.ro;
+                    // a resumed ray's is a chord direction (no start window: NaN gives 0)
+                    RECORD ? r.rd : F3(NAN, NAN, NAN), fr.max_dphi);
 #ifdef SR_STATS_FIRE
     bs.fires = 0;
     struct Out {

@@ -58,8 +58,9 @@ print("value", d["value"], "ms", d["ms_per_step"], "frac", rf.get("frac"), "pari
 PY
     ;;
   rocstats)
-    export GPU_MAX_HW_QUEUES=8
-    step rocstats 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python $DRIVER --cpu-baseline off ${BENCH_ARGS:-}
+    # the queue count scoped to this step (a temporary assignment on the
+    # function call), so later steps keep the box default
+    GPU_MAX_HW_QUEUES=8 step rocstats 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python $DRIVER --cpu-baseline off ${BENCH_ARGS:-}
     find "$OUT/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$OUT/kernel_stats.csv"
     grep '^{' "$OUT/rocstats.log" > "$OUT/rocstats_bench.json" || true
     head -4 "$OUT/kernel_stats.csv" | cut -c1-200 ;;
@@ -89,11 +90,10 @@ SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_IN
       python tools/pmc_summary.py "$OUT/pmc_$v"
     done ;;
   traffic)
-    export GPU_MAX_HW_QUEUES=8
     B="bench.py --steps 8 --warmup 4 --cpu-baseline off --critical-path off --reference-loop off --single-frame off"
     for n in $TRAFFIC; do
       for c in FETCH_SIZE WRITE_SIZE; do
-        SR_LIB=$V/libsr_$n.so step "traffic_${n}_$c" 180 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$n-$c" -o run --output-format csv -- python $B
+        GPU_MAX_HW_QUEUES=8 SR_LIB=$V/libsr_$n.so step "traffic_${n}_$c" 180 rocprofv3 --kernel-trace --pmc $c -d "$OUT/$n-$c" -o run --output-format csv -- python $B
       done
       python tools/traffic_json.py --frame "$OUT/$n-FETCH_SIZE" "$OUT/$n-WRITE_SIZE" --out "$OUT/traffic_$n.json" > "$OUT/traffic_$n.log" 2>&1 \
         || { cat "$OUT/traffic_$n.log"; exit 1; }
