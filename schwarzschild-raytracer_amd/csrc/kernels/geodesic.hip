@@ -94,64 +94,7 @@ struct Tex {
     const uint8_t* __restrict__ opq;  // texture-array opacity bitmap (sr_api.cpp make_opacity_map)
 };
 
-// budget slots 0 .. 8 have their own counters in measurement builds
-#define SR_STATS_SLOTS 9
-#ifdef SR_STATS
-// Measurement builds only: wave-level event counters (tools/stats_frame.py).
-//   0 wave-steps  1 budget events  2..10 slot j reached (exact chord)
-//   11 -  12 exact object tests run  13 lane-steps  14..22 slot j spent
-__device__ unsigned long long sr_stats[64];
-// per-wave [start, end] s_memrealtime (100 MHz) of sr_integrate_kernel, by wave index
-#define SR_WAVE_LOG (1 << 17)
-#define SR_WAVE_REC 16  // t0, t1, max steps, events << 32 | exact chords, reach count of slots 0..8
-__device__ unsigned long long sr_wave_t[SR_WAVE_REC * SR_WAVE_LOG];
-__device__ __forceinline__ void stat_add(int k, unsigned long long v) {
-    const unsigned long long act = __ballot(1);
-    if ((int)__lane_id() == __builtin_ctzll(act)) atomicAdd(&sr_stats[k], v);
-}
-#ifdef SR_STATS_NOCOUNT  // timeline only: the counters' atomics distort it
-#define SR_STAT(k, v) ((void)0)
-#else
-#define SR_STAT(k, v) stat_add(k, v)
-#endif
-#else
-#define SR_STAT(k, v) ((void)0)
-#endif
-
-#ifdef SR_LANE_MASK
-// Latency experiments only: a per-pixel keep mask (device pointer) over the full frame
-__device__ const uint8_t* sr_lane_mask;
-#endif
-
-#ifdef SR_PROF
-// Measurement builds only (tools/prof_waves.py): per-wave shader-clock cycles
-// by section of the step loop, wave-uniform accumulators (no per-lane state,
-// so the build keeps the production register allocation as far as possible).
-//   0 fast loop  1 reseeds  2 slow-path entry + approximate chord  3 budget events phase 1
-//   4 exact chord + intersect  5 hit classification + log  6 budget events phase 2  7 wave total
-#define SR_PROF_N 24  // 0-6 sections, 7 wave total | max steps << 48, 8-15 re-anchors of budget slots 0-7,
-                      // 22 budget_init, 23 kernel start to integrate (launch code, pixel, ray set-up),
-                      // 16 budget events, 17 events spending only slot 0, 18 lanes spending slot 0 (sum),
-                      // 19 slow-path entries, 20 event phase 1 up to the spent ballots (the rest
-                      // in 3), 21 slow-path tail + top of the step loop (2: exit to the event)
-__device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
-#define SR_PT(k)                                                      \
-    do {                                                              \
-        const unsigned t_ = (unsigned)clock64();                      \
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[k] += t_ - prof_t_; \
-        prof_t_ = t_;                                                 \
-    } while (0)
-// the same inside budget_event (accumulators reached through the Budget)
-#define SR_PTB(k)                                                     \
-    do {                                                              \
-        const unsigned t_ = (unsigned)clock64();                      \
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[k] += t_ - *bs.pt; \
-        *bs.pt = t_;                                                  \
-    } while (0)
-#else
-#define SR_PT(k) ((void)0)
-#define SR_PTB(k) ((void)0)
-#endif
+#include "probes.h"
 
 // ---- primitive tests: return the reference's is_hit and fill p ------------
 // sphere_intersect, frag:457-478 (r2: the float square r * r of the radius):
@@ -812,13 +755,7 @@ struct Budget {
     // the inner window (uhi in (SR_BH_U, 1): sr_dev_frame.bh_u2 / bh_u3)
     static __device__ __forceinline__ bool inner(float uhi) { return uhi > SR_BH_U && uhi < 1.0f; }
     static __device__ __forceinline__ float ulo_of(float uhi, float u_f) { return inner(uhi) ? SR_BH_ULO2 : u_f; }
-#ifdef SR_STATS_FIRE  // measurement builds only: steps that ran any exact test
-    int fires;
-#endif
-#ifdef SR_PROF
-    unsigned* prof;
-    unsigned* pt;
-#endif
+    SR_PROBE_BUDGET_FIELDS  // measurement builds only (probes.h)
 };
 
 // The orbital frame's projections (pa, pb) on the budgeted cylinders' axes.
@@ -1219,16 +1156,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     // below stay scalar loads in every build (pin_slot's SGPR constraints)
     spent = __builtin_amdgcn_readfirstlane(spent);
     SR_PTB(20);
-#ifdef SR_PROF
-    {
-        const unsigned long long b0 = __ballot(!(T < e[0]) || (forced & 1u));
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) {
-            bs.prof[16] += 1;
-            bs.prof[17] += spent == 1u;
-            bs.prof[18] += __popcll(b0);
-        }
-    }
-#endif
+    SR_PROBE(probe_event_phase1(bs, T, e[0], forced, spent));
     // the others run on: charge them the path since the last event
     float m = INFINITY, mh = INFINITY;
 #pragma unroll
@@ -1261,9 +1189,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
         if (j <= 8) SR_STAT(14 + j, 1);
-#ifdef SR_PROF
-        if (j < 8 && (threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) bs.prof[8 + j] += 1;
-#endif
+        SR_PROBE(if (j < 8) SR_PROF_BUMP(bs.prof, 8 + j, 1));
         // only lanes whose budget did not cover the chord can reach the slot
         // (the others re-anchor early: look-ahead, or another lane spent it)
         // (its E is still the uncharged one in LDS: spent slots are only written below)
@@ -1919,13 +1845,7 @@ struct Ray {
     f3 ro, rd, nv, tv;
     float u, du;
     int i, steps;
-#ifdef SR_PROF
-    unsigned* prof;  // the wave's 8 section accumulators in LDS
-#endif
-#ifdef SR_STATS
-    int ev, mat;  // budget events, exact chords (measurement builds)
-    int rc[SR_STATS_SLOTS];
-#endif
+    SR_PROBE_RAY_FIELDS  // measurement builds only (probes.h)
 };
 
 struct Pix {
@@ -2016,11 +1936,7 @@ __device__ __forceinline__ int init_pixel(const sr_dev_frame& fr, const sr_dev_c
     r.nv = nrm(r.ro);
     r.steps = 0;
     r.i = 0;
-#ifdef SR_STATS
-    r.ev = 0;
-    r.mat = 0;
-    for (int j = 0; j < SR_STATS_SLOTS; j++) r.rc[j] = 0;
-#endif
+    SR_PROBE(probe_ray_init(r));
     const bool flat = fr.raytrace_type == SR_RAYTRACE_FLAT ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_WIDTH && uv.x > 2.0f * fr.curved_percentage + -1.0f) ||
                       (fr.raytrace_type == SR_RAYTRACE_HALF_HEIGHT && uv.y > 2.0f * fr.curved_percentage + -1.0f);
@@ -2155,9 +2071,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     __shared__ float lds_E[BS::L::ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     BS bs;
     bs.E = lds_E + threadIdx.x;
-#ifdef SR_PROF
-    const unsigned prof_bi_ = (unsigned)clock64();  // budget_init's cycles (section 22)
-#endif
+    SR_PROBE(SR_PROF_CLOCK(prof_bi_));  // budget_init's cycles (section 22)
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
         budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
@@ -2166,14 +2080,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     // the ray's start (sr_integrate_kernel): r.rd is the orbit's tangent at r.ro;
                     // a resumed ray's is a chord direction (no start window: NaN gives 0)
                     RECORD ? r.rd : F3(NAN, NAN, NAN), fr.max_dphi);
-#ifdef SR_STATS_FIRE
-    bs.fires = 0;
-    struct Out {
-        Ray& r;
-        BS& b;
-        __device__ ~Out() { r.steps = b.fires; }
-    } out_{r, bs};
-#endif
+    SR_PROBE(FireProbe<Ray, BS> fire_probe_(r, bs));
     const int N = fr.max_steps;
     // every chord is tested exactly when objects outside the budget slots or
     // the test rays are present (wave-uniform)
@@ -2214,16 +2121,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     };
     bool force = false;  // this lane's next chord is charged exactly (new orbital frame)
     int i = r.i;
-#ifdef SR_STATS
-    int last_ev = i;
-    int near_run = 0;
-#endif
-#ifdef SR_PROF
-    unsigned prof_t_ = (unsigned)clock64();
-    bs.prof = r.prof;
-    bs.pt = &prof_t_;
-    if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[22] += prof_t_ - prof_bi_;
-#endif
+    SR_PROBE(LoopProbe lp(i); SR_PROF_LOOP_START(r, bs, prof_bi_));
     for (;;) {
         if (RECORD) i = __builtin_amdgcn_readfirstlane(i);  // every lane started at step 0: keep i scalar
         // (sr_resume_kernel's lanes are unrelated rays at their own steps)
@@ -2338,9 +2236,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 vb = __builtin_fmaf(__builtin_fmaf(q, un, __builtin_fmaf(bt, e.w, bn * e.z)), un, 1.0f);
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
-#if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
-                if (CM) SR_STAT(31, 1);  // wave-steps of the cylinder-plane fast loop
-#endif
+                SR_PROBE(if (CM) SR_STAT_MAIN(31, 1));  // wave-steps of the cylinder-plane fast loop
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
             };
             // apply step i and move to entry en of step i + 1
@@ -2453,24 +2349,16 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         else fast(I0{});
         SR_PT(0);
         if (i >= N) {
-#if defined(SR_STATS_STEPHIST)  // measurement only: recover_up's replayed steps (end of loop)
-            SR_STAT(56, N - 1 - ick);
-            SR_STAT(57, 1);
-#endif
+            SR_PROBE(SR_STAT_STEPHIST(56, N - 1 - ick); SR_STAT_STEPHIST(57, 1));  // recover_up's replayed steps
             up = recover_up(N);
             break;
         }
-#ifdef SR_PROF
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[19] += 1;
-#endif
+        SR_PROBE(SR_PROF_BUMP(r.prof, 19, 1));
         // ---- slow path of step i
         r.i = i;
         r.steps = sbase + i + 1;
         if (un < 0.0f) {
-#if defined(SR_STATS_STEPHIST)  // measurement only: recover_up's replayed steps (u < 0 exit)
-            if (i > ick) SR_STAT(58, i - 1 - ick);
-            SR_STAT(59, 1);
-#endif
+            SR_PROBE(if (i > ick) SR_STAT_STEPHIST(58, i - 1 - ick); SR_STAT_STEPHIST(59, 1));  // (u < 0 exit)
             up = recover_up(i);
             settle_prev(i);
             return ST_BG;
@@ -2541,151 +2429,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                     bs.setC(cx, cy);
                 }
                 SR_STAT(1, 1);
-#ifdef SR_STATS
-                r.ev++;
-                {  // steps since the wave's previous event, lanes that triggered it (tools/stats_frame.py)
-                    const int iv = i - last_ev;
-                    last_ev = i;
-                    SR_STAT(32 + (iv <= 1 ? 0 : iv <= 3 ? 1 : iv <= 7 ? 2 : iv <= 15 ? 3 : iv <= 63 ? 4 : 5), 1);
-                    const int nl = __popcll(__ballot(event));
-                    SR_STAT(38 + (nl <= 1 ? 0 : nl <= 3 ? 1 : nl <= 7 ? 2 : nl <= 15 ? 3 : nl <= 31 ? 4 : 5), 1);
-#if defined(SR_STATS_STEPHIST)  // measurement only (tools/stats_frame.py --stephist): events by step
-                    {
-                        // events (44 + b) and their triggering lanes (50 + b) by the step
-                        // index's bucket b: < 25, < 100, < 300, < 700, < 1200, the rest
-                        const int bk = i < 25 ? 0 : i < 100 ? 1 : i < 300 ? 2 : i < 700 ? 3 : i < 1200 ? 4 : 5;
-                        SR_STAT(44 + bk, 1);
-                        SR_STAT(50 + bk, nl);
-                    }
-#elif defined(SR_STATS_NEAR)
-                    // measurement only (tools/stats_frame.py --near): back-to-back events
-                    {
-                        // slots some lane has spent at this event (bit j), by interval 1 (44..46:
-                        // one, two, three or more slots) and longer (47..49); runs of consecutive
-                        // interval-1 events, recorded when a longer interval ends one (50..54:
-                        // 1, 2-3, 4-7, 8-15, 16+); interval-1 events spending one slot, by slot (55..61)
-                        const float Tt = bs.T();
-                        uint32_t sm = 0;
-                        for (int j = 0; j < 7; j++) {
-                            const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
-                            if (__ballot(!(Tt < ej))) sm |= 1u << j;
-                        }
-                        const int ns = __popc(sm);
-                        SR_STAT((iv <= 1 ? 44 : 47) + (ns <= 1 ? 0 : ns == 2 ? 1 : 2), 1);
-                        if (iv <= 1) {
-                            near_run++;
-                            if (ns == 1) SR_STAT(55 + __builtin_ctz(sm), 1);
-                        } else if (near_run > 0) {
-                            SR_STAT(50 + (near_run <= 1 ? 0 : near_run <= 3 ? 1 : near_run <= 7 ? 2 : near_run <= 15 ? 3 : 4), 1);
-                            near_run = 0;
-                        }
-                    }
-#elif defined(SR_STATS_TRIG)  // measurement only (tools/stats_frame.py --trig): who spends which slot
-                    {
-                        // lanes whose own budget of slot j ran out (44 + j: orbiting the
-                        // photon sphere, 51 + j: the others) and events that re-anchor
-                        // slot j by the look-ahead alone (58 + j)
-                        const bool ring = r.u > 0.5f && r.u < 0.95f && fabsf(r.du) < 0.15f;
-                        const float Tt = bs.T();
-                        for (int j = 0; j < 7; j++) {
-                            const float ej = j <= sc->num_budget ? bs.E[j * SR_E_STRIDE] : INFINITY;
-                            const bool own = !(Tt < ej);
-                            SR_STAT(44 + j, __popcll(__ballot(own && ring)));
-                            SR_STAT(51 + j, __popcll(__ballot(own && !ring)));
-                            if (j < 6 && __ballot(!(Tt + ahead < ej)) && !__ballot(own)) SR_STAT(58 + j, 1);
-                        }
-                    }
-#elif defined(SR_STATS_XCYL)  // measurement only (tools/stats_frame.py --xcyl): the cylinder's spends by plane distance
-                    if (sc->budget_cyl_mask) {
-                        // lanes spending the first budgeted cylinder (44), of them those whose orbital
-                        // plane is farther than br + d from its bounding centre, d = 0.25, 1, 2, 4
-                        // (45..48); events spending it (49), spending it alone (54), and alone with
-                        // only such lanes (50..53)
-                        const int jc = __builtin_ctz((uint32_t)sc->budget_cyl_mask) + 1;
-                        const sr_dev_slot& sl = sc->slots[jc - 1];
-                        const float Tt = bs.T();
-                        uint32_t sm = 0;
-                        for (int j = 0; j <= sc->num_budget; j++)
-                            if (__ballot(!(Tt < bs.E[j * SR_E_STRIDE]))) sm |= 1u << j;
-                        const bool own = !(Tt < bs.E[jc * SR_E_STRIDE]);
-                        const f3 n = cross(r.nv, r.tv);
-                        const float h = fabsf(dot(ld3(sl.bc), n)) * __builtin_amdgcn_rsqf(dot(n, n)) - sl.br;
-                        const float dd[4] = {0.25f, 1.0f, 2.0f, 4.0f};
-                        SR_STAT(44, __popcll(__ballot(own)));
-                        if (__ballot(own)) SR_STAT(49, 1);
-                        if (sm == (1u << jc)) SR_STAT(54, 1);
-                        for (int k = 0; k < 4; k++) {
-                            SR_STAT(45 + k, __popcll(__ballot(own && h > dd[k])));
-                            if (sm == (1u << jc) && !__ballot(own && !(h > dd[k]))) SR_STAT(50 + k, 1);
-                        }
-                    }
-#else
-                    if (!__ballot(!(vb < 0.0f))) SR_STAT(44, 1);  // the black hole's u window alone
-                    SR_STAT(45, __popcll(__ballot(event && !(q0 < INFINITY))));  // lanes whose ball was empty
-                    SR_STAT(46, __popcll(__ballot(bhx)));
-                    SR_STAT(47, nl);
-                    if (iv <= 1) {
-                        SR_STAT(48, nl >= 32);
-                        SR_STAT(49, __popcll(__ballot(event && !(q0 < INFINITY))));
-                        SR_STAT(50, nl);
-                        SR_STAT(51, __popcll(__ballot(event && reseeded)));
-                        SR_STAT(52, __popcll(__ballot(event && bs.m() < 0.05f)));
-                        SR_STAT(53, any_cm);
-                        {  // the slot holding the smallest budget of each triggering lane
-                            int jm = 0;
-                            float em = bs.E[0];
-                            for (int j = 1; j <= sc->num_budget; j++) {
-                                const float v = bs.E[j * SR_E_STRIDE];
-                                if (v < em) { em = v; jm = j; }
-                            }
-                            for (int j = 0; j <= 8; j++) SR_STAT(55 + j, __popcll(__ballot(event && jm == j && em < 0.05f)));
-                        }
-                    }
-                    SR_STAT(54, any_cm);
-#endif
-                }
-#endif
+                SR_PROBE(probe_event(sc, bs, r, lp, i, event, vb, q0, bhx, reseeded, ahead, any_cm));
                 // sr_wave_costs: the wave's event count (one lane, its own LDS word)
                 if (WCOST && (int)__lane_id() == __builtin_ctzll(__ballot(1)))
                     sr_lds_ev[threadIdx.x >> 6] += 1;
                 // a new frame (reseed): the cylinders' direction tests start over
                 SR_PT(2);
-#ifdef SR_STATS_BH  // measurement only (tools/stats_bh.py): the black hole's triggering lanes by orbit state
-                {
-                    const bool h0 = !(bs.T() < bs.E[0]);
-                    const bool ring = r.u <= 0.9f && r.u > 0.55f && fabsf(r.du) < 0.1f;
-                    SR_STAT(23, __popcll(__ballot(h0 && r.u > 1.0f)));
-                    SR_STAT(24, __popcll(__ballot(h0 && r.u <= 1.0f && r.u > 0.9f)));
-                    SR_STAT(25, __popcll(__ballot(h0 && ring)));
-                    SR_STAT(26, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && r.du > 0.0f)));
-                    SR_STAT(27, __popcll(__ballot(h0 && r.u <= 0.9f && !ring && !(r.du > 0.0f))));
-                    SR_STAT(28, __popcll(__ballot(event)));
-                    SR_STAT(29, __popcll(__ballot(h0)));
-                    SR_STAT(30, __ballot(h0) != 0ull);
-                    SR_STAT(31, __popcll(__ballot(1)));
-                }
-#endif
-#ifdef SR_STATS_DIR  // measurement only (tools/stats_dir.py): object triggers by the lane's radial direction
-                {
-                    const bool outw = r.du < 0.0f && r.u < 0.6f;
-                    const bool inc = r.du > 0.0f;
-                    bool any = false;
-#pragma unroll
-                    for (int j = 1; j <= 6; j++) {
-                        const bool h = !(bs.T() < bs.E[j * SR_E_STRIDE]);
-                        any |= h;
-                        if (j == 3 || j == 5) {  // the default scene's accretion disk and rectangle
-                            const int b = j == 3 ? 23 : 26;
-                            SR_STAT(b, __popcll(__ballot(h && outw)));
-                            SR_STAT(b + 1, __popcll(__ballot(h && inc)));
-                            SR_STAT(b + 2, __popcll(__ballot(h && !outw && !inc)));
-                        }
-                    }
-                    SR_STAT(29, __popcll(__ballot(any && outw)));
-                    SR_STAT(30, __popcll(__ballot(any && inc)));
-                    SR_STAT(31, __popcll(__ballot(any)));
-                }
-#endif
                 // the inner window's bound for this lane: steep falling lanes get bh_u3
                 const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
                 reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
@@ -2693,20 +2442,12 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                                      fr.u_f, fr.bh_u2, fr.bh_u3, steep);
                 if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
                 SR_PT(6);
-#ifdef SR_STATS
-                for (uint32_t c = reach & 0x1ffu; c; c &= c - 1) SR_STAT(2 + __builtin_ctz(c), 1);
-#pragma unroll
-                for (int j = 0; j < SR_STATS_SLOTS; j++) r.rc[j] += (reach >> j) & 1u;
-#endif
+                SR_PROBE(probe_reach(r, reach));
                 if (!__ballot(reach != 0u || every)) break;
-#ifdef SR_STATS_FIRE
-                bs.fires++;
-#endif
+                SR_PROBE(probe_fire(bs));
             }
             // frag:924-930: the exact chord of step i
-#ifdef SR_STATS
-            r.mat++;
-#endif
+            SR_PROBE(probe_exact_chord(r));
             f3 prev = im == i - 1 ? r.ro : point_at(r, up, p1.x, p1.y);
             r.ro = point_at(r, r.u, e.z, e.w);
             im = i;
@@ -2872,19 +2613,9 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
 #else
     if (order && wg < SR_PRIO_BLOCKS) __builtin_amdgcn_s_setprio(3);
 #endif
-#ifdef SR_STATS
-    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long c_start = __builtin_amdgcn_s_memtime();  // shader clock: the in-kernel clock (rec[15])
-    unsigned long long evmat = 0;
-    int rcv[SR_STATS_SLOTS] = {};
-#endif
+    SR_PROBE(WaveProbe wp);  // measurement builds only (probes.h)
     Pix q;
     int steps = 0;
-#ifdef SR_PROF
-    __shared__ unsigned prof_lds[SR_WG / 64][SR_PROF_N];
-    if ((threadIdx.x & 63) < SR_PROF_N) prof_lds[threadIdx.x >> 6][threadIdx.x & 63] = 0;
-    const unsigned long long prof_t0 = clock64();
-#endif
     if (WCOST && (threadIdx.x & 63) == 0) sr_lds_ev[threadIdx.x >> 6] = 0;
     if (tid >= 0 && pixel_of(fr, block, tid, q)) {
         sr_lds_pid[threadIdx.x] = (uint32_t)(((size_t)frame * (size_t)fr.tiles + (size_t)block) * 256 + tid);
@@ -2897,22 +2628,11 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         Ray r;
         Hit hit;
         int st = init_pixel(fr, fr.cam[frame], q, r);
-#ifdef SR_LANE_MASK  // latency experiments only (tools/lane_mask.py): masked pixels run no ray
-        if (sr_lane_mask && !sr_lane_mask[(size_t)q.py * fr.width + q.px]) st = ST_DONE;
-#endif
-#ifdef SR_PROF
-        r.prof = prof_lds[threadIdx.x >> 6];
-        if ((threadIdx.x & 63) == __builtin_ctzll(__ballot(1))) r.prof[23] += (unsigned)(clock64() - prof_t0);
-#endif
+        SR_PROBE(st = wp.lane_mask(q.px, q.py, fr.width, st, ST_DONE); wp.ray_start(r));
         if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
-#if defined(SR_STATS) && !defined(SR_STATS_BH) && !defined(SR_STATS_DIR)
-        // pixels, logged hits, pixels by status (tools/stats_frame.py; wave sums)
-        SR_STAT(23, __popcll(__ballot(1)));
-        SR_STAT(24, __popcll(__ballot(log.n & 1)) + 2 * __popcll(__ballot(log.n & 2)) + 4 * __popcll(__ballot(log.n & 4)));
-        for (int k = 0; k < 6; k++) SR_STAT(25 + k, __popcll(__ballot(st == k)));
-#endif
+        SR_PROBE(wp.pixel(st, log.n));
         if (st == ST_FLAT || st == ST_MORE) ps.put3(PS_RO, id, r.ro);
         if (st == ST_MORE) {  // resumable (sr_resume_kernel)
             ps.puti(PS_I, id, r.i);
@@ -2922,51 +2642,9 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
             ps.at(PS_DU, id) = r.du;
         }
         steps = r.steps;
-#ifdef SR_STATS
-        evmat = ((unsigned long long)r.ev << 32) | (unsigned)r.mat;
-        for (int j = 0; j < SR_STATS_SLOTS; j++) rcv[j] = r.rc[j];
-#endif
+        SR_PROBE(wp.ray_end(r));
     }
-#ifdef SR_STATS
-    {
-        int sm = steps;
-        unsigned long long em = evmat;
-        for (int off = 32; off > 0; off >>= 1) {
-            sm = max(sm, __shfl_xor(sm, off));
-            const unsigned long long o = __shfl_xor(em, off);
-            em = o > em ? o : em;
-        }
-        int rcm[SR_STATS_SLOTS];
-        for (int j = 0; j < SR_STATS_SLOTS; j++) {
-            rcm[j] = rcv[j];
-            for (int off = 32; off > 0; off >>= 1) rcm[j] = max(rcm[j], __shfl_xor(rcm[j], off));
-        }
-        const int w = (frame * fr.tiles + block) * 4 + (ttid >> 6);
-        if ((threadIdx.x & 63) == 0 && w < SR_WAVE_LOG) {
-            unsigned long long* rec = sr_wave_t + (size_t)SR_WAVE_REC * w;
-            rec[0] = t_start;
-            rec[1] = __builtin_amdgcn_s_memrealtime();
-            rec[2] = (unsigned long long)sm;
-            rec[3] = em;
-            for (int j = 0; j < SR_STATS_SLOTS; j++) rec[4 + j] = (unsigned long long)rcm[j];
-            rec[13] = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-            rec[14] = __builtin_amdgcn_s_getreg((31 << 11) | 4);  // HW_REG_HW_ID (wave, SIMD, CU, SE)
-            rec[15] = __builtin_amdgcn_s_memtime() - c_start;     // shader-clock cycles of the wave
-        }
-    }
-#endif
-#ifdef SR_PROF
-    {
-        const int w = block * 4 + (ttid >> 6);
-        int sm = steps;
-        for (int off = 32; off > 0; off >>= 1) sm = max(sm, __shfl_xor(sm, off));
-        if ((threadIdx.x & 63) == 0 && w < (1 << 17)) {
-            unsigned long long* rec = sr_prof + (size_t)SR_PROF_N * w;
-            for (int k = 0; k < SR_PROF_N; k++) rec[k] = prof_lds[threadIdx.x >> 6][k];
-            rec[7] = (clock64() - prof_t0) | ((unsigned long long)sm << 48);
-        }
-    }
-#endif
+    SR_PROBE(wp.finish(frame, fr.tiles, block, ttid, steps));
     if (cost) {  // all 64 lanes are active here
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) steps = max(steps, __shfl_xor(steps, off));
@@ -3244,49 +2922,3 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }
-
-#ifdef SR_PROF
-extern "C" int sr_debug_prof(unsigned long long* out, int n_waves) {
-    if (n_waves < 0 || n_waves > (1 << 17)) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_prof), SR_PROF_N * (size_t)n_waves * sizeof(unsigned long long)) !=
-        hipSuccess)
-        return -3;
-    return 0;
-}
-#endif
-
-#ifdef SR_LANE_MASK
-extern "C" int sr_debug_set_lane_mask(const uint8_t* dev_mask) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(sr_lane_mask), &dev_mask, sizeof dev_mask) == hipSuccess ? 0 : -3;
-}
-#endif
-
-#ifdef SR_STATS
-// Measurement builds only: read (and clear) the kernel's event counters.
-extern "C" int sr_debug_stats(unsigned long long* out32) {
-    if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
-    unsigned long long z[32] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z) != hipSuccess) return -3;
-    return 0;
-}
-// counters 32..63 (read and cleared): event intervals and triggering lanes
-extern "C" int sr_debug_stats_hi(unsigned long long* out32) {
-    if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(sr_stats), 32 * sizeof(unsigned long long), 32 * sizeof(unsigned long long)) !=
-        hipSuccess)
-        return -3;
-    unsigned long long z[32] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(sr_stats), z, sizeof z, 32 * sizeof(unsigned long long)) != hipSuccess) return -3;
-    return 0;
-}
-extern "C" int sr_debug_wave_times(unsigned long long* out, int n_waves) {
-    if (n_waves < 0 || n_waves > SR_WAVE_LOG) return -1;
-    if (hipDeviceSynchronize() != hipSuccess) return -3;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(sr_wave_t), SR_WAVE_REC * (size_t)n_waves * sizeof(unsigned long long)) !=
-        hipSuccess)
-        return -3;
-    return 0;
-}
-#endif

@@ -52,8 +52,12 @@ CONFIGS = {
     # with the press-R overlay's 1000-point polyline
     "c2s": (640, 360, 1000, "2k"),
     "c2t": (640, 360, 1000, "2k"),
+    # the same at the headline size (round 6: bench.py --scene stress /
+    # --test-ray on at 1920x1080 / 2000 steps)
+    "c3s": (1920, 1080, 2000, "2k"),
+    "c3t": (1920, 1080, 2000, "2k"),
 }
-VARIANTS = {"c2s": "stress", "c2t": "testray"}  # the others: "default"
+VARIANTS = {"c2s": "stress", "c2t": "testray", "c3s": "stress", "c3t": "testray"}  # the others: "default"
 CHUNK = 16
 
 
