@@ -161,6 +161,9 @@ def parse():
                          "of pixels of this rank's share per launch, at most half of --steps)")
     ap.add_argument("--split", default="0",
                     help="split tiles MAX_TILES[:LANES[:MIN_STEPS]] (sr_set_split; 0: off)")
+    ap.add_argument("--stream-priority", choices=["off", "lead"], default="off",
+                    help="lead: the first context's stream at high priority, the others at normal priority "
+                         "(the hardware dispatches the leading launch's workgroups first; the others fill in)")
     ap.add_argument("--balance", choices=["auto", "cost", "cyclic"], default="auto",
                     help="N > 1: cost: each rank renders an equal number of 8-row blocks of about equal cost "
                          "(dist.balanced_blocks over the frame's step map, sr_render_block_list); cyclic: block b "
@@ -376,8 +379,12 @@ def main():
         tile_k = torch.zeros((B, D.tile_rows(world, H, BLOCK_ROWS), W, 4), dtype=torch.uint8, device=dev)
         host_k = torch.zeros(tuple(tile_k.shape), dtype=torch.uint8).pin_memory() if gloo else None
         gather_k = D.FrameGather(host_k if gloo else tile_k, world, rank, H, BLOCK_ROWS)
-        ctxs.append((rk, tile_k, gather_k, torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev),
-                     host_k))
+        if args.stream_priority == "lead":
+            lo, hi = torch.cuda.Stream.priority_range()  # (lowest, highest): lower numbers run first
+            s_k = torch.cuda.Stream(dev, priority=hi if k == 0 else lo)
+        else:
+            s_k = torch.cuda.current_stream(dev) if k == 0 else torch.cuda.Stream(dev)
+        ctxs.append((rk, tile_k, gather_k, s_k, host_k))
     r, tile, _, stream, _ = ctxs[0]
 
     frames = {}  # --dump-frames: frame index -> assembled frame (rank 0), timed frames only
@@ -712,6 +719,7 @@ def main():
                 "last_camera_max_over_mean": last_camera,
                 "dist_backend": args.dist_backend if distributed else None,
                 "launches_in_flight": F,
+                "stream_priority": args.stream_priority,
                 "frames_per_launch": B,
                 "frames_in_flight": F * B,
                 # the timed window's launches (frames each): a window that is

@@ -2550,7 +2550,7 @@ constexpr int sr_integrate_waves(int nb, int nc) {
                               : (nb > SR_NB_SMALL || nc > SR_NC_SMALL) ? SR_GENERAL_WAVES_PER_EU : SR_MIN_WAVES_PER_EU;
 }
 
-// Launch codes (sr_order_kernel): tile << 8 for a whole 16x16 workgroup tile;
+// Launch codes (order_tiles): tile << 8 for a whole 16x16 workgroup tile;
 // tile << 8 | SR_SPLIT | sub for workgroup `sub` of a split tile; -1 for an
 // unused slot of the grid.
 #define SR_SPLIT 0x80
@@ -2577,7 +2577,7 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 
 // 1-D grid: workgroup s = (slot * B + f) * SR_WG_PER_TILE + part renders
 // part `part` (SR_WG threads) of launch code order[slot] of frame f of the
-// batch (costliest tiles of every frame first, sr_order_kernel), and records
+// batch (costliest tiles of every frame first, order_tiles), and records
 // the tile's cost (max steps of its rays over the batch).
 // WCOST: the sr_wave_costs instantiation (per-wave steps and events to
 // fr.wave_cost); the frame kernels carry none of its code.
@@ -2679,11 +2679,17 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
 // streams rarely left free, and its stream waited up to 6.5 ms behind it
 // (mean 0.35 ms per launch, profiles/r04/s6_kernel_stats.csv).
 #define SR_ORDER_WG 256
-__global__ __launch_bounds__(SR_ORDER_WG) void sr_order_kernel(int* __restrict__ cost, int n, int max_cost,
-                                                        int* __restrict__ order, int split_tiles, int split_log2,
-                                                        int split_min) {
+// Round 6: one workgroup of the shade kernel (the grid's first, so it is
+// dispatched before the shading ones) instead of a kernel of its own after
+// it: the launch order of the next frame is off this frame's critical path
+// (a frame alone spent 0.038 ms in the resume and order kernels after its
+// shade kernel, tools/frame_parts.py), and the buckets' offsets are a
+// parallel scan instead of one thread's loop over the 256 buckets.
+__device__ __forceinline__ void order_tiles(int* __restrict__ cost, int n, int max_cost, int* __restrict__ order,
+                                            int split_tiles, int split_log2, int split_min) {
     __shared__ int hist[256];
     __shared__ int offs[256];
+    __shared__ int wsum[SR_ORDER_WG / 64];
     __shared__ int nsplit;
     const int t = threadIdx.x;
     // 256 cost buckets, descending cost = descending bucket. With split
@@ -2699,19 +2705,27 @@ __global__ __launch_bounds__(SR_ORDER_WG) void sr_order_kernel(int* __restrict__
         else b = (long long)c * 128 / smin;
         return (int)(b < 0 ? 0 : b > 255 ? 255 : b);
     };
-    if (t < 256) hist[t] = 0;
+    hist[t] = 0;
     __syncthreads();
     for (int i = t; i < n; i += SR_ORDER_WG) atomicAdd(&hist[bucket(cost[i])], 1);
     __syncthreads();
-    if (t == 0) {
-        int run = 0, hi = 0;
-        for (int b = 255; b >= 0; b--) {
-            offs[b] = run;
-            run += hist[b];
-            if (b >= 128) hi += hist[b];
-        }
-        nsplit = split_tiles < hi ? split_tiles : hi;
+    // thread t holds bucket 255 - t (descending cost): an inclusive scan over
+    // the threads gives each bucket's end, its exclusive prefix its offset
+    const int lane = t & 63, wv = t >> 6;
+    const int h = hist[255 - t];
+    int x = h;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
     }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < wv; k++) base += wsum[k];
+    offs[255 - t] = base + x - h;
+    // tiles in the top half of the buckets (cost >= split_min with split tiles)
+    if (t == 127) nsplit = split_tiles < base + x ? split_tiles : base + x;
     __syncthreads();
     const int S = 64 >> split_log2;  // split workgroups per tile
     const int ns = nsplit;
@@ -2726,6 +2740,12 @@ __global__ __launch_bounds__(SR_ORDER_WG) void sr_order_kernel(int* __restrict__
     }
     for (int j = n + (S - 1) * ns + t; j < n + (S - 1) * split_tiles; j += SR_ORDER_WG) order[j] = -1;
 }
+// the next frame's launch order (order_tiles) in the shade kernel's first workgroup
+struct OrderArgs {
+    int* cost;
+    int* order;
+    int n, max_cost, split_tiles, split_log2, split_min;
+};
 
 #ifndef SR_SHADE_WAVES_PER_EU
 #define SR_SHADE_WAVES_PER_EU 1
@@ -2738,8 +2758,16 @@ __global__ __launch_bounds__(256, SR_SHADE_WAVES_PER_EU) void sr_shade_kernel(co
                                                       uint8_t* __restrict__ out, size_t pitch,
                                                       float* __restrict__ dbg_rgba, int32_t* __restrict__ dbg_steps,
                                                       int* __restrict__ list, int* __restrict__ count,
-                                                      int* __restrict__ diag) {
-    const int vblock = blockIdx.y * gridDim.x + blockIdx.x;  // frame f's tiles are rows f*gy .. of the grid
+                                                      int* __restrict__ diag, OrderArgs oa) {
+    // with a launch order to compute, grid row 0 is its workgroup's (block
+    // (0, 0)) and the frames' tiles follow in rows 1 ..
+    const int row0 = oa.order ? 1 : 0;
+    if ((int)blockIdx.y < row0) {
+        if (blockIdx.x == 0)
+            order_tiles(oa.cost, oa.n, oa.max_cost, oa.order, oa.split_tiles, oa.split_log2, oa.split_min);
+        return;
+    }
+    const int vblock = ((int)blockIdx.y - row0) * gridDim.x + blockIdx.x;  // frame f's tiles are rows f*gy ..
     const int f = vblock / fr.tiles, block = vblock - f * fr.tiles;
     Pix q;
     if (!pixel_of(fr, block, threadIdx.x, q)) return;
@@ -2852,7 +2880,7 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
 }
 
 // order/cost (optional, one int per workgroup tile): the launch order and
-// the cost feedback of sr_order_kernel
+// the cost feedback of order_tiles
 extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
                                          const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
                                          const sr_dev_frame* fr, uint8_t* out, size_t pitch, float* dbg_rgba,
@@ -2866,7 +2894,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     if (B < 1 || B > SR_MAX_BATCH || fr->tiles != (int)nblocks) return hipErrorInvalidValue;
     if ((size_t)nblocks * B * 256 > ps_n || (size_t)nblocks * B * 256 > (size_t)INT32_MAX) return hipErrorInvalidValue;
     if ((order == nullptr) != (cost == nullptr)) return hipErrorInvalidValue;
-    // split tiles need the launch order (their codes come from sr_order_kernel)
+    // split tiles need the launch order (their codes come from order_tiles)
     const int split = order ? fr->split_tiles : 0;
     if (split < 0 || (split && (fr->split_log2 < 0 || fr->split_log2 > 4 || (fr->split_log2 & 1))))
         return hipErrorInvalidValue;
@@ -2903,8 +2931,9 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
         hipLaunchKernelGGL((sr_integrate_kernel<false, false, 1, SR_FAST_UNROLL, 1>), dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
     if (ev4) (void)hipEventRecord(ev4[1], stream);
-    hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B), block, 0, stream, sc, segs, bg, arr, *fr, ps, ps_n,
-                       out, pitch, dbg_rgba, dbg_steps, list, count, diag);
+    OrderArgs oa{cost, order, (int)nblocks, fr->max_steps, split, split ? fr->split_log2 : 6, fr->split_min_steps};
+    hipLaunchKernelGGL(sr_shade_kernel, dim3(grid.x, grid.y * B + (order ? 1u : 0u)), block, 0, stream, sc, segs, bg,
+                       arr, *fr, ps, ps_n, out, pitch, dbg_rgba, dbg_steps, list, count, diag, oa);
     if (ev4) (void)hipEventRecord(ev4[2], stream);
 #ifndef SR_RESUME_TILES  // the resume kernel's grid-stride grid, in 256-thread tiles
 #define SR_RESUME_TILES 1024u
@@ -2916,9 +2945,6 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     else
         hipLaunchKernelGGL(sr_resume_kernel<false>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
-    if (order)
-        hipLaunchKernelGGL(sr_order_kernel, dim3(1), dim3(SR_ORDER_WG), 0, stream, cost, (int)nblocks, fr->max_steps, order,
-                           split, split ? fr->split_log2 : 6, fr->split_min_steps);
     if (ev4) (void)hipEventRecord(ev4[3], stream);
     return hipGetLastError();
 }

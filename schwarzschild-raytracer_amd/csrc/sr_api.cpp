@@ -68,7 +68,7 @@ struct sr_ctx {
     int* d_count = nullptr;
     size_t ps_n = 0;
     // workgroup-tile launch order (costliest first) and per-tile cost of the
-    // last frame, one pair per grid shape (geodesic.hip sr_order_kernel): kept
+    // last frame, one pair per grid shape (geodesic.hip order_tiles): kept
     // for the context's lifetime, so a shape change never frees a buffer an
     // in-flight frame still reads
     struct Order {
@@ -568,7 +568,7 @@ void evict_orders(sr_ctx* ctx) {
 // Launch order for a grid shape: tiles nearest the frame centre first (where
 // the black hole usually is) until a frame has measured the costs. One
 // buffer pair per shape and split setting, allocated on first use. Entries
-// are launch codes (geodesic.hip sr_order_kernel): tile << 8 for a whole
+// are launch codes (geodesic.hip order_tiles): tile << 8 for a whole
 // tile, -1 for the split grid's slots no tile uses yet.
 int ensure_order(sr_ctx* ctx, int gx, int gy, const int* list, hipStream_t s, int** order, int** cost) {
     const int split = ctx->split_tiles;
@@ -1355,7 +1355,7 @@ int sr_set_latency_mode(sr_ctx* c, int on) {
     return SR_OK;
 }
 
-// Not in sr.h's public set: the launch codes sr_order_kernel wrote at the end
+// Not in sr.h's public set: the launch codes order_tiles wrote at the end
 // of the context's last frame (the next frame of that shape runs them; tile
 // << 8, | 0x80 | sub for split workgroups, -1 unused). Waits for the frame.
 int sr_debug_last_order(sr_ctx* c, int* out, int max_n, int* n) {
