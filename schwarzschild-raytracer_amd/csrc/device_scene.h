@@ -220,9 +220,9 @@ typedef struct {
     // sqrt(8 (1 - out_dip)), rounded up: at least the step angle (the budget
     // events' directional plane window, geodesic.hip plane_window)
     float max_dphi;
-    // fast-loop steps per iteration of the integrate kernel: 3, or 2 in the
-    // latency mode (sr_set_latency_mode: one frame alone ~5 % sooner, frames
-    // in flight ~0.5 % slower)
+    // fast-loop steps per iteration of the integrate kernel:
+    // SR_FAST_UNROLL_DEFAULT, or 2 in the latency mode (sr_set_latency_mode;
+    // DESIGN.md §7)
     int32_t fast_unroll;
     // S_max = (sqrt 3 + 3) R + 1 (x 1.001, rounded up) for R = 1 / u_f: bounds
     // |o|_1 + len + 1 of every chord from inside the u_f sphere to within 2 R
@@ -249,6 +249,10 @@ typedef struct {
 // (under the photon orbit's 4/27: such an orbit outside the photon sphere
 // stays at u <= 0.58, so |u'| <= sqrt(E) and |u''| <= 1/6 along it)
 #define SR_XCYL_EMAX 0.14f
+
+// the integrate kernel's default fast-loop steps per iteration (geodesic.hip
+// SR_FAST_UNROLL)
+#define SR_FAST_UNROLL_DEFAULT 4
 // the largest step angle (max_angle / max_steps, here max_dphi) at which the
 // low-energy exclusions apply (sr_api.cpp clear_radius): their premises (E
 // conserved within 2 %, one step moving u by at most kappa, u never past the

@@ -592,8 +592,10 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #define SR_AHEAD 2.0f
 #endif
 #ifndef SR_FAST_UNROLL  // fast-loop steps per iteration (1 .. 4; the step table has 4 padding entries);
-                        // the latency mode's instantiation runs 2 (sr_set_latency_mode)
-#define SR_FAST_UNROLL 3
+                        // the latency mode's instantiation runs 2 (sr_set_latency_mode). 4 since round 6:
+                        // at 7 waves per SIMD 0.5 % more frames per second than 3 in two A/Bs
+                        // (profiles/r06/s18, s19), one frame alone level
+#define SR_FAST_UNROLL SR_FAST_UNROLL_DEFAULT
 #endif
 #ifndef SR_AHEAD_T
 #define SR_AHEAD_T 1.0f

@@ -93,7 +93,7 @@ struct sr_ctx {
     hipStream_t upload = nullptr;
     // split tiles (sr_set_split): 0 = off
     int split_tiles = 0, split_log2 = 4, split_min_steps = 1;
-    int fast_unroll = 3;  // sr_set_latency_mode: 2
+    int fast_unroll = SR_FAST_UNROLL_DEFAULT;  // sr_set_latency_mode: 2
     const int* last_order = nullptr;  // the launch codes of the context's last frame (its next frame's order)
     size_t last_slots = 0;
     // the stream of the context's last launch: a context is used from one
@@ -1351,7 +1351,7 @@ int sr_set_split(sr_ctx* c, int max_tiles, int lanes_per_wave, int min_steps) {
 
 int sr_set_latency_mode(sr_ctx* c, int on) {
     if (!c) return SR_E_INVALID;
-    c->fast_unroll = on ? 2 : 3;
+    c->fast_unroll = on ? 2 : SR_FAST_UNROLL_DEFAULT;
     return SR_OK;
 }
 
