@@ -642,7 +642,7 @@ struct BudgetLayout {
 // no distance budget for the hole: its slot-0 budget is +inf and the step
 // loop exits on u > uhi = SR_BH_U instead (one compare per step), where slot
 // 0 re-anchors and the chord is reach-tested. Lanes inside the band (or the
-// shell) keep the distance budget, uhi = +inf. Ring rays orbit the photon
+// shell) keep the distance budget, uhi = SR_U_NOWIN. Ring rays orbit the photon
 // sphere at r ~ 1.5 for hundreds of steps: their distance budgets (0.5 at r =
 // 1.5) ran out every ~50 steps per lane and made the hole the most frequent
 // event (profiles/r03/s19_*: its re-anchors 186 k -> 93 k per headline frame,
@@ -651,6 +651,15 @@ struct BudgetLayout {
 #define SR_BH_WINDOW 1
 #endif
 #define SR_BH_U 0.986f      // u at r = 1.01420
+// A lane without a window keeps uhi = the largest float below 1e30, not
+// +inf: a ray through the singularity (u past 1e30, then +inf, where RK4
+// keeps u = u' = +inf) leaves the fast loop there for the slow path's
+// degenerate chord (integrate: degen; the reference's chord of zero length
+// and NaN direction ends the ray). Its ball test alone does not catch it: a
+// ball around the origin holds every such end point (vb -> -inf). Round 6:
+// a stress-scene ray that passed the shell behind an alpha-0 texel ran on to
+// max_steps (found once that scene's lazy chords were switched on).
+#define SR_U_NOWIN 0x1.93e592p+99f
 #define SR_BH_RWIN 1.0143f  // an anchor beyond this radius (by perr) starts a window
 // The inner window (SR_BH_WINDOW2): chords whose two ends both lie at r in
 // [1.00402, 1.1] (u in [SR_BH_ULO2, 0.996]) with a step angle below 0.063
@@ -729,7 +738,7 @@ struct Budget {
     //   mh  min_k of the cylinders' slab budgets H[k] (E[SLAB0 + k]): the bound
     //       that covers chords nearly parallel to an axis
     //   cm  budgeted cylinders (bit k) whose axis this orbital plane may nearly contain
-    //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; +inf: none; bh_u2 /
+    //   uhi the step loop's exit bound on u for the black hole (SR_BH_WINDOW; SR_U_NOWIN: none; bh_u2 /
     //       bh_u3: the inner window, whose lower bound is SR_BH_ULO2 instead of u_f: ulo_of())
     __device__ __forceinline__ float ld(int row) const { return E[row * SR_E_STRIDE]; }
     __device__ __forceinline__ void st(int row, float v) const { E[row * SR_E_STRIDE] = v; }
@@ -889,7 +898,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
     uint32_t xcl = 0;
     {
         float e = clearance_bh(a);
-        float uhi = INFINITY;
+        float uhi = SR_U_NOWIN;
         if (SR_BH_WINDOW && bh_ok && a > SR_BH_RWIN) {
             e = INFINITY;
             uhi = SR_BH_U;
@@ -1205,7 +1214,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
             const bool win2 = SR_BH_WINDOW2 && dip > SR_BH_DIP2 && (a - perr) * uw > 1.000001f &&
                               a + perr < SR_BH_RMAX2 && (falling || !win1);
             const bool win = win1 || win2;
-            bs.setUhi(win2 ? uw : win1 ? SR_BH_U : INFINITY);
+            bs.setUhi(win2 ? uw : win1 ? SR_BH_U : SR_U_NOWIN);
             const float v = (win || (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)))
                                 ? INFINITY
                                 : clearance_bh(a) - perr;
@@ -2239,6 +2248,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_STAT(0, 1);
                 SR_STAT(13, __popcll(__ballot(1)));
                 SR_PROBE(if (CM) SR_STAT_MAIN(31, 1));  // wave-steps of the cylinder-plane fast loop
+                SR_PROBE(if (!(un < 1.0e20f)) SR_TRACE_AT("fast i=%d u=%g un=%g dun=%g vb=%g q=%g\n", i, r.u, un,
+                                                            dun, vb, q));
                 return __ballot(!(vb < 0.0f) || un < ulo || un > uhi);
             };
             // apply step i and move to entry en of step i + 1
@@ -2375,6 +2386,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // arithmetic hits, so every slot is tested (reach below)
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
+        SR_PROBE(SR_TRACE_AT("slow i=%d u=%.9g un=%.9g uhi=%.9g vb=%g force=%d event=%d bhx=%d m=%g\n", i, r.u, un,
+                             uhi, vb, (int)force, (int)event, (int)bhx, bm));
 #ifndef SR_BH_CROSS
 #define SR_BH_CROSS 1
 #endif
@@ -2445,6 +2458,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
                 SR_PT(6);
                 SR_PROBE(probe_reach(r, reach));
+                SR_PROBE(SR_TRACE_AT("  event reach=%x uhi'=%.9g m'=%g E0=%g\n", reach, bs.uhi(), bs.m(), bs.ld(0)));
                 if (!__ballot(reach != 0u || every)) break;
                 SR_PROBE(probe_fire(bs));
             }
@@ -2458,6 +2472,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             r.rd = delta / seg;
             hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
             SR_PT(4);
+            SR_PROBE(SR_TRACE_AT("  chord i=%d seg=%g slot=%d\n", i, seg, hit.slot));
             if (hit.slot != SLOT_NONE) {
                 const int op = hit_opacity(sc, fr, tx, hit, -r.rd, !RECORD);
                 SR_PT(5);

@@ -78,6 +78,13 @@ __device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
 #else
 #define SR_PROBE(...)
 #endif
+// SR_TRACE (with SR_LANE_MASK, one unmasked pixel): device printf of the
+// slow path's steps, events and hits of the rays that run (post-mortems)
+#ifdef SR_TRACE
+#define SR_TRACE_AT(...) printf(__VA_ARGS__)
+#else
+#define SR_TRACE_AT(...)
+#endif
 // the first active lane of the wave (the one that updates wave-level accumulators)
 #define SR_LEAD() ((int)(threadIdx.x & 63) == (int)__builtin_ctzll(__ballot(1)))
 // a counter only the default statistics build keeps (the SR_STATS_BH / _DIR

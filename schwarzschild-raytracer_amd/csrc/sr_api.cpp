@@ -175,6 +175,65 @@ void set_bound(sr_dev_obj& o, V3 c, float R, int kind, float mu) {
     o.pl1 = l1norm(ld(o.f + SR_F_POS));
 }
 
+// The accepted region of rect_test (frag:573-584) for a frame that need not
+// be orthonormal: the points pos + q with c1 . q = 0 (the plane through pos
+// with normal c1), 0 <= c0 . q <= w and 0 <= c2 . q <= h, a parallelogram
+// with the corners q = M^-1 (alpha, 0, beta) for M's rows c0, c1, c2.
+// Appends its corners (binary64); kappa = |M|_F |M^-1|_F >= the condition
+// number, which scales the rounding of an accepted point's position. False
+// for a singular or non-finite frame.
+bool parallelogram_corners(V3 pos, V3 c0, V3 c1, V3 c2, float w, float h, std::vector<std::array<double, 3>>& out,
+                           double& kappa) {
+    const double m[3][3] = {{c0.x, c0.y, c0.z}, {c1.x, c1.y, c1.z}, {c2.x, c2.y, c2.z}};
+    const double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) -
+                       m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                       m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    if (!std::isfinite(det) || std::fabs(det) < 1e-6 || !(w >= 0.f) || !(h >= 0.f)) return false;
+    double inv[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const int i1 = (j + 1) % 3, i2 = (j + 2) % 3, j1 = (i + 1) % 3, j2 = (i + 2) % 3;
+            inv[i][j] = (m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1]) / det;  // adjugate / det
+        }
+    double fm = 0, fi = 0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            fm += m[i][j] * m[i][j];
+            fi += inv[i][j] * inv[i][j];
+        }
+    kappa = std::sqrt(fm * fi);
+    for (int k = 0; k < 4; k++) {
+        const double al = (k & 1) ? w : 0.0, be = (k & 2) ? h : 0.0;  // M q = (al, 0, be)
+        std::array<double, 3> q;
+        for (int i = 0; i < 3; i++) q[i] = (double)(&pos.x)[i] + inv[i][0] * al + inv[i][2] * be;
+        out.push_back(q);
+    }
+    return std::isfinite(kappa);
+}
+
+// Bounding sphere of a non-orthonormal rectangle's or box's accepted region
+// (the parallelograms of its faces): budgeted like an orthonormal one but by
+// that sphere alone (mp = +inf: no distance-to-primitive refinement, no
+// directional plane window), its planar margin factor scaled by the frame's
+// condition number. A scene with such an object no longer tests every chord
+// exactly (round 6: the max-capacity scene's skewed rectangle had turned
+// lazy chords off for the whole frame).
+bool set_bound_corners(sr_dev_obj& o, const std::vector<std::array<double, 3>>& pts, double kappa) {
+    if (pts.empty() || !(kappa < 1e3)) return false;
+    double c[3] = {0, 0, 0};
+    for (const auto& q : pts)
+        for (int i = 0; i < 3; i++) c[i] += q[i] / (double)pts.size();
+    double R = 0;
+    for (const auto& q : pts)
+        R = std::max(R, std::sqrt((q[0] - c[0]) * (q[0] - c[0]) + (q[1] - c[1]) * (q[1] - c[1]) +
+                                  (q[2] - c[2]) * (q[2] - c[2])));
+    const V3 cf = v3((float)c[0], (float)c[1], (float)c[2]);
+    const double slack = 1e-5 * (std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2]) + R);  // the centre's rounding
+    set_bound(o, cf, (float)((R + slack) * (1.0 + 1e-6)), SR_KIND_BUDGET, (float)(SR_MU_PLANAR * std::max(1.0, kappa)));
+    o.mp = INFINITY;  // the frame's distances are not Euclidean: the bounding sphere alone
+    return o.kind == SR_KIND_BUDGET;
+}
+
 void put_transform(float* f, const sr_transform& t) {
     std::memcpy(f + SR_F_POS, t.pos, 3 * sizeof(float));
     std::memcpy(f + SR_F_AXES, t.axes, 9 * sizeof(float));
@@ -271,6 +330,11 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
         if (orthonormal(a0, a1, a2) && w >= 0.f && h >= 0.f) {
             V3 c = add(ld(f), add(scl(a0, 0.5f * w), scl(a2, 0.5f * h)));
             set_bound(o, c, (float)std::sqrt(0.25 * w * w + 0.25 * h * h), SR_KIND_BUDGET, SR_MU_PLANAR);
+        } else {
+            std::vector<std::array<double, 3>> pts;
+            double kappa = 0;
+            o.kind = SR_KIND_EXACT;
+            if (parallelogram_corners(ld(f), a0, a1, a2, w, h, pts, kappa)) set_bound_corners(o, pts, kappa);
         }
         return SR_OK;
     }
@@ -300,6 +364,18 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
             double R = 0.5 * std::sqrt((double)b.width * b.width + (double)b.height * b.height +
                                        (double)b.depth * b.depth);
             set_bound(o, c, (float)R, SR_KIND_BUDGET, SR_MU_PLANAR);
+        } else {
+            // the six faces' parallelograms (box_intersect tests each face's rect_test)
+            std::vector<std::array<double, 3>> pts;
+            double kappa = 1, kf = 0;
+            bool ok = true;
+            o.kind = SR_KIND_EXACT;
+            for (int fc = 0; fc < 6 && ok; fc++) {
+                const float* g = F + fc * S;
+                ok = parallelogram_corners(ld(g), ld(g + 3), ld(g + 6), ld(g + 9), g[12], g[13], pts, kf);
+                kappa = std::max(kappa, kf);
+            }
+            if (ok) set_bound_corners(o, pts, kappa);
         }
         return SR_OK;
     }

@@ -443,6 +443,61 @@ def test_random_scenes_culling_exact(pkg, gpu, seed):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("shear", [0.0, 0.3, -0.6])
+@pytest.mark.parametrize("scale", [1.3, 0.7])
+def test_skewed_frames_budgeted(pkg, gpu, oracle, oracle_tex, shear, scale):
+    """Rectangles and boxes whose frames are not orthonormal (a column scaled,
+    a shear between columns) are budgeted by the bounding sphere of their
+    faces' parallelograms since round 6 (sr_api.cpp parallelogram_corners;
+    they were tested on every chord and turned lazy chords off for the whole
+    frame): the default scene with its rectangle and box so skewed, whole
+    frames bit-exact against the oracle, and culling on vs off identical."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = sc.scene_default(textured=True)
+    A = np.eye(3)
+    A[:, 0] *= scale
+    A[:, 2] += shear * A[:, 1]
+    cols = [float(np.float32(v)) for v in A.T.reshape(-1)]  # column-major axes
+    for k in range(9):
+        scene.rectangles[0].plane.transform.axes[k] = cols[k]
+        scene.boxes[0].transform.axes[k] = cols[(k + 3) % 9]
+    cam = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0), fov=70.0)
+    params = abi.default_params(max_steps=1200, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, cam, params, 160, 90)
+    o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
+    print(compare(g, o, f"skewed frames, scale {scale}, shear {shear}"))
+    outs = []
+    for cull in (True, False):
+        gpu.set_culling(cull)
+        f, b, st = gpu.render_debug(cam, params, 160, 90)
+        torch.cuda.synchronize()
+        outs.append((f.cpu().numpy().view(np.uint32), b.cpu().numpy(), st.cpu().numpy()))
+    gpu.set_culling(True)
+    for a, b_ in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b_)
+
+
+def test_ray_through_singularity(pkg, gpu, oracle, oracle_tex):
+    """A ray that passes the r = 1 shell behind an alpha-0 texel (the chord's
+    closest hit is the object, so the hole is not hit) falls on to the
+    singularity: u passes 1e30, then +inf, where RK4 keeps u = u' = +inf, and
+    the reference's next chord (zero length, NaN direction) ends the ray with
+    a NaN colour at step 285. The fast loop must leave for that degenerate
+    chord although the lane's ball holds the origin (geodesic.hip SR_U_NOWIN;
+    round 6: the stress scene's pixel (322, 154) at 640x360 ran to max_steps
+    once that scene's chords were lazy)."""
+    sc, abi = pkg.scenes, pkg.abi
+    params = abi.default_params(max_steps=1000, percent_black=-1.0)
+    cam = abi.default_camera()
+    g = gpu_debug(gpu, sc.scene_stress(), cam, params, 640, 360, row_begin=152, row_end=157)
+    o = oracle.render(sc.scene_stress(), cam, params, 640, 360, oracle_tex, row_begin=152, row_end=157)
+    assert o[2][154 - 152, 322] == 285  # the case is the one described
+    assert np.isnan(o[1][154 - 152, 322]).any()
+    print(compare(g, o, "ray through the singularity"))
+
+
 def test_test_ray_far_view(pkg, gpu, oracle, oracle_tex):
     """A visible press-R polyline seen from far away: every chord must be
     tested against the test-ray cylinders even where no budget is spent."""
