@@ -2385,6 +2385,29 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // length, NaN direction) and the exact tests decide what its NaN
         // arithmetic hits, so every slot is tested (reach below)
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
+        // Past the singularity: u before and after the step both +inf or NaN.
+        // RK4 keeps u there (inf + x is inf or NaN, NaN stays NaN) and no
+        // compare of the loop fires (u < 0, u < u_f, the hole's window), so
+        // the reference runs on to max_steps, and every chord from here has
+        // both ends at +-0 or NaN (point_at divides by u): length 0 or NaN,
+        // direction 0 / 0 or NaN / x, NaN in all three components. Each
+        // primitive test then misses whatever its origin: sphere_test's and
+        // cyl_test's discriminant is NaN (not < 0) and so are their roots
+        // (lam stays -1 / in1, in2 false); plane_test's denominator is NaN
+        // (not < eps) and so is lam (not >= 0), which fails the disks,
+        // rectangles and boxes too. So the ray ends at max_steps with no
+        // further hit and a final direction of three NaNs, whose get_bg
+        // (bilinear's s = t = 0 for any NaN, whatever its sign or payload)
+        // is the loop's: end it here. The stress scene's rays through an
+        // object's translucent skin at the shell ran ~1800 such steps, each
+        // an event with every slot tested (round 6: its single frame
+        // 31 -> see DESIGN.md §7).
+        if (CULL && !(r.u < INFINITY) && !(un < INFINITY)) {
+            r.i = N;
+            r.steps = sbase + N;
+            r.rd = F3(NAN, NAN, NAN);
+            return ST_BG;
+        }
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
         SR_PROBE(SR_TRACE_AT("slow i=%d u=%.9g un=%.9g uhi=%.9g vb=%g force=%d event=%d bhx=%d m=%g\n", i, r.u, un,
                              uhi, vb, (int)force, (int)event, (int)bhx, bm));

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-wave cycle breakdown of sr_integrate_kernel by step-loop section, from
 an SR_PROF build (tools/build_variant.sh NAME -DSR_PROF):
-  python tools/prof_waves.py lib/variants/libsr_NAME.so [--rows 704 720] [--scene tex]
+  python tools/prof_waves.py lib/variants/libsr_NAME.so [--rows 704 720] [--scene tex|untex|bh|stress]
 Sections: fast loop, reseeds, slow-path entry + approximate chord, budget
 events, exact chord + intersect, hit classification + log."""
 import argparse
@@ -37,7 +37,8 @@ def main():
     lib.sr_debug_prof.restype = C.c_int
     lib.sr_debug_prof.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     r = pkg.Renderer(0)
-    r.set_scene(sc.scene_black_hole_only() if args.scene == "bh" else sc.scene_default(textured=args.scene == "tex"))
+    r.set_scene(sc.scene_black_hole_only() if args.scene == "bh" else sc.scene_stress() if args.scene == "stress"
+                else sc.scene_default(textured=args.scene == "tex"))
     r.set_background(sc.skybox(2048, 1024))
     arr, _, _ = sc.default_texture_array()
     r.set_texture_array(arr)

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Event counters of an SR_STATS build (tools/build_variant.sh NAME -DSR_STATS):
 renders the headline frame once and prints the step loop's wave-level counts.
-  python tools/stats_frame.py lib/variants/libsr_NAME.so [--scene tex|untex|bh]"""
+  python tools/stats_frame.py lib/variants/libsr_NAME.so [--scene tex|untex|bh|stress]"""
 import argparse
 import ctypes as C
 import json
@@ -40,6 +40,8 @@ def main():
     r = pkg.Renderer(0)
     if args.scene == "bh":
         r.set_scene(sc.scene_black_hole_only())
+    elif args.scene == "stress":
+        r.set_scene(sc.scene_stress())
     else:
         r.set_scene(sc.scene_default(textured=args.scene == "tex"))
     r.set_background(sc.skybox(2048, 1024))
