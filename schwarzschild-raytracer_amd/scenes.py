@@ -236,10 +236,12 @@ def scene_random(seed: int, n_objects: int = 21, translucent: bool = True, plane
 
 # The bench's max-capacity scene (bench.py --scene stress; BASELINE.md / the
 # verdict's "what the default scene hides"): every capacity of the uniform
-# block filled (frag:63-182): 3 of each primitive (21 objects, more than the
-# kernel's SR_MAX_BUDGET budget slots, so 13 are tested per chord), 10
-# materials, 4 lights. Fixed seed: tests/golden/frame_hashes.npz holds its
-# oracle frame (config "c2s").
+# block filled (frag:63-182): 3 of each primitive (21 objects, all of them
+# budget slots of the large integrate instantiation, SR_MAX_BUDGET = 21; its
+# skewed rectangle by the bounding sphere of its parallelogram since round 6,
+# sr_api.cpp set_bound_corners), 10 materials, 4 lights. Fixed seed:
+# tests/golden/frame_hashes.npz holds its oracle frames (configs "c2s" at
+# 640x360 / 1000 steps, "c3s" at the headline 1920x1080 / 2000).
 STRESS_SEED = 2024
 
 

@@ -97,9 +97,10 @@ def frame_digest(rgba8):
 
 
 def test_fixture_covers_the_configs(fh):
-    """configs 2-5 and config 2's stress / test-ray variants in full (every
-    row), each with its frame hash"""
-    for cfg, H in (("c2", 360), ("c3", 1080), ("c4", 2160), ("c5", 4320), ("c2s", 360), ("c2t", 360)):
+    """configs 2-5 and the stress / test-ray variants of configs 2 and 3 in
+    full (every row), each with its frame hash"""
+    for cfg, H in (("c2", 360), ("c3", 1080), ("c4", 2160), ("c5", 4320), ("c2s", 360), ("c2t", 360),
+                   ("c3s", 1080), ("c3t", 1080)):
         assert len(fh[f"{cfg}/rows"]) == H, cfg
         assert f"{cfg}/frame_sha" in fh, cfg
 
@@ -262,14 +263,16 @@ def test_frame_gather_device_reassembly(pkg, fh, assets):
     r.close()
 
 
-@pytest.mark.parametrize("cfg,variant", [("c2s", "stress"), ("c2t", "testray")])
+@pytest.mark.parametrize("cfg,variant", [("c2s", "stress"), ("c2t", "testray"), ("c3s", "stress"),
+                                         ("c3t", "testray")])
 def test_variant_frames_exact(pkg, fh, assets, cfg, variant):
-    """What the default scene hides, at config 2's size (bench.py --scene
-    stress / --test-ray on): the max-capacity scene (21 objects, 13 of them
-    tested per chord beside the 8 budget slots; 10 materials, 4 lights) and
-    the default scene with the press-R overlay's 1000-point polyline (1000
-    cylinders against every chord). The debug render (steps) and two batched
-    launches, every row against the oracle's hashes."""
+    """What the default scene hides, at config 2's size and at the headline's
+    (bench.py --scene stress / --test-ray on): the max-capacity scene (21
+    objects, every one a budget slot of the large instantiation; 10
+    materials, 4 lights) and the default scene with the press-R overlay's
+    1000-point polyline (1000 cylinders against every chord). The debug
+    render (steps) and two batched launches, every row against the oracle's
+    hashes."""
     import torch
 
     W, H, N = (int(v) for v in fh[f"{cfg}/config"])
