@@ -221,14 +221,29 @@ def spawn_ranks(n: int, argv: list[str], grace_s: float = 30.0) -> int:
     order the ranks failed), else 0; once a rank has failed the others get
     `grace_s` to finish before they are terminated (they would otherwise wait
     in a collective for the dead rank)."""
+    # free_port() closes its socket before rank 0's store binds the port, so
+    # another process can take it in between: rank 0 then exits with
+    # EXIT_PORT_TAKEN (main) and the ranks are started again on a new port
+    for attempt in range(PORT_ATTEMPTS):
+        rc = _run_ranks(n, argv, free_port(), grace_s)
+        if rc != EXIT_PORT_TAKEN:
+            return rc
+        print(f"bench: rendezvous port taken (attempt {attempt + 1}), new port", file=sys.stderr)
+    return rc
+
+
+EXIT_PORT_TAKEN = 98  # errno EADDRINUSE: rank 0's rendezvous store could not bind MASTER_PORT
+PORT_ATTEMPTS = 3
+
+
+def _run_ranks(n: int, argv: list[str], port: int, grace_s: float) -> int:
     import signal
 
-    port = free_port()
     script = str(Path(__file__).resolve())
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SR_BENCH_SPAWNED="1")
         procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
 
     def stop(*_):
@@ -250,6 +265,8 @@ def spawn_ranks(n: int, argv: list[str], grace_s: float = 30.0) -> int:
                 if rc not in (None, 0) and first_bad == 0:
                     first_bad, failed_at = rc, time.monotonic()
                     print(f"bench: rank {procs.index(p)} exited with status {rc}", file=sys.stderr)
+                    if rc == EXIT_PORT_TAKEN:  # the others wait on a store that never came up
+                        failed_at -= grace_s
             if failed_at is not None and time.monotonic() - failed_at > grace_s:
                 stop()
                 break
@@ -262,6 +279,13 @@ def spawn_ranks(n: int, argv: list[str], grace_s: float = 30.0) -> int:
         stop()
         signal.signal(signal.SIGTERM, old)
     return 1 if first_bad < 0 else first_bad  # a signal-killed rank (negative rc) is a failure too
+
+
+def port_taken(e: BaseException) -> bool:
+    """Whether an init_process_group failure is the store's bind of a port
+    another process holds (EADDRINUSE)."""
+    msg = str(e).lower()
+    return "address already in use" in msg or "eaddrinuse" in msg or "errno: 98" in msg
 
 
 def launch_contract(args) -> None:
@@ -325,11 +349,17 @@ def main():
     ndev = max(1, ndev_seen)
     dev = torch.device("cuda", local % ndev)
     if distributed:
-        if args.dist_backend == "nccl":
-            torch.cuda.set_device(dev)
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        try:
+            if args.dist_backend == "nccl":
+                torch.cuda.set_device(dev)
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group("gloo")
+        except Exception as e:
+            if port_taken(e) and os.environ.get("SR_BENCH_SPAWNED") == "1" and rank == 0:
+                print(f"bench: rank 0 could not bind MASTER_PORT: {e}", file=sys.stderr)
+                sys.exit(EXIT_PORT_TAKEN)  # spawn_ranks retries on a new port
+            raise
 
     # ---- inputs resident in HBM ---------------------------------------------------
     scene = sc.scene_stress() if args.scene == "stress" else sc.scene_default(textured=True)

@@ -40,8 +40,10 @@
 #include <cstring>
 #include <ctime>
 #include <fstream>
-#include <sys/stat.h>
+#include <sstream>
 #include <string>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <thread>
 #include <vector>
 
@@ -220,23 +222,53 @@ void setup_slot(Slot& s, int dev, const Args& a, const sr_scene& scene, size_t t
 // One process per GPU: the file through which rank 0 hands the RCCL unique id
 // to the other ranks. --id-file, else a name unique to the launch: the
 // launcher's run id (TORCHELASTIC_RUN_ID) and rendezvous port (MASTER_PORT),
-// so concurrent or earlier runs with other ports never share a file. Ranks > 0
-// also reject a file older than themselves (main's stat check), and rank 0
-// removes it once every rank has joined.
-constexpr time_t kIdSkewS = 30;  // launcher start-up skew allowed between ranks
-
-static std::string id_file_path(const std::string& given) {
-    if (!given.empty()) return given;
+// so concurrent runs with other ports never share a file; with neither (and
+// no --id-file) a multi-process run is refused (plain-env launches
+// all shared one name). A file with this launch's name but written before the
+// launcher that started this rank (a crashed earlier run on the same port) is
+// rejected by its modification time against the parent process's start
+// (parent_start), whatever the ranks' own start-up skew; rank 0 removes the
+// file once every rank has joined.
+static bool id_file_path(const std::string& given, std::string& path) {
+    if (!given.empty()) {
+        path = given;
+        return true;
+    }
     const char* run = std::getenv("TORCHELASTIC_RUN_ID");
     const char* port = std::getenv("MASTER_PORT");
-    std::string p = "/tmp/sr_multi_gpu";
-    if (run && *run && std::strcmp(run, "none") != 0) p += std::string(".") + run;
-    if (port && *port) p += std::string(".") + port;
-    return p + ".ncclid";
+    const bool has_run = run && *run && std::strcmp(run, "none") != 0, has_port = port && *port;
+    path = "/tmp/sr_multi_gpu";
+    if (has_run) path += std::string(".") + run;
+    if (has_port) path += std::string(".") + port;
+    path += ".ncclid";
+    return has_run || has_port;
+}
+
+// The start time (seconds since the epoch) of this process's parent - the
+// launcher that started every rank of the run - from /proc (field 22 of
+// /proc/<ppid>/stat in clock ticks after boot, /proc/stat's btime); -1 when
+// unknown (then only the file name separates runs).
+static double parent_start() {
+    std::ifstream st("/proc/" + std::to_string(::getppid()) + "/stat");
+    std::string line;
+    if (!std::getline(st, line)) return -1.0;
+    const size_t close = line.rfind(')');  // the command name may hold spaces
+    if (close == std::string::npos) return -1.0;
+    std::istringstream rest(line.substr(close + 2));
+    std::string f;
+    unsigned long long ticks = 0;
+    for (int k = 3; k <= 22 && (rest >> f); k++)
+        if (k == 22) ticks = std::strtoull(f.c_str(), nullptr, 10);
+    std::ifstream ps("/proc/stat");
+    unsigned long long btime = 0;
+    while (std::getline(ps, line))
+        if (line.compare(0, 6, "btime ") == 0) btime = std::strtoull(line.c_str() + 6, nullptr, 10);
+    const long hz = ::sysconf(_SC_CLK_TCK);
+    if (!ticks || !btime || hz <= 0) return -1.0;
+    return (double)btime + (double)ticks / (double)hz;
 }
 
 int main(int argc, char** argv) {
-    const time_t t_start = std::time(nullptr);
     Args a = parse(argc, argv);
     const char* ws = std::getenv("WORLD_SIZE");
     const bool per_process = ws && std::atoi(ws) > 1;
@@ -282,18 +314,26 @@ int main(int argc, char** argv) {
     if (per_process) {
         devs[0].dev = local % ndev;
         ncclUniqueId id;
-        const std::string path = id_file_path(a.id_file);
+        std::string path;
+        if (!id_file_path(a.id_file, path)) {
+            std::fprintf(stderr, "rank %d: WORLD_SIZE > 1 needs --id-file, MASTER_PORT or TORCHELASTIC_RUN_ID "
+                                 "(a name no other launch shares)\n", rank);
+            return 1;
+        }
         if (rank == 0) {
             CHECK_NCCL(ncclGetUniqueId(&id));
             const std::string tmp = path + ".tmp";
             std::ofstream(tmp, std::ios::binary).write(reinterpret_cast<const char*>(&id), sizeof id);
             std::rename(tmp.c_str(), path.c_str());
         } else {
-            // a file older than this process (minus the launcher's start-up
-            // skew) is a previous run's: never hand its id to ncclCommInitRank
+            // a file written before this run's launcher started is a previous
+            // run's: never hand its id to ncclCommInitRank (btime is whole
+            // seconds, so the launcher's start is known to within 1 s)
+            const double launched = parent_start();
             for (int t = 0;; t++) {
                 struct stat st;
-                if (::stat(path.c_str(), &st) == 0 && st.st_mtime + kIdSkewS >= t_start) {
+                if (::stat(path.c_str(), &st) == 0 &&
+                    (launched < 0.0 || (double)st.st_mtim.tv_sec + 1e-9 * (double)st.st_mtim.tv_nsec >= launched - 1.0)) {
                     std::ifstream f(path, std::ios::binary);
                     if (f.read(reinterpret_cast<char*>(&id), sizeof id)) break;
                 }

@@ -148,6 +148,47 @@ def test_spawn_ranks_env_and_status(tmp_path):
         bench.__file__ = old
 
 
+def test_spawn_ranks_retries_a_taken_port(tmp_path):
+    """free_port() releases its socket before rank 0's store binds
+    the port. A rank 0 that finds it taken exits with EXIT_PORT_TAKEN and
+    spawn_ranks starts every rank again on a new port; the real store's error
+    on a held port is what `port_taken` recognises."""
+    import os
+    import socket
+
+    import bench
+
+    probe = tmp_path / "probe.py"
+    probe.write_text("import os, sys\n"
+                     f"d = r'{tmp_path}'\n"
+                     "n = len([f for f in os.listdir(d) if f.startswith('try')])\n"
+                     "if os.environ['RANK'] == '0':\n"
+                     "    open(os.path.join(d, 'try%d_' % n + os.environ['MASTER_PORT']), 'w').close()\n"
+                     "    sys.exit(98 if n == 0 else 0)\n")
+    old = bench.__file__
+    try:
+        bench.__file__ = str(probe)
+        assert bench.spawn_ranks(2, [], grace_s=60) == 0
+    finally:
+        bench.__file__ = old
+    tries = sorted(p.name for p in tmp_path.iterdir() if p.name.startswith("try"))
+    assert len(tries) == 2 and tries[0].split("_")[1] != tries[1].split("_")[1]
+    # the store's own message for a port another socket holds
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        s.listen(1)
+        code = ("import datetime, os, torch.distributed as d\n"
+                "try:\n"
+                "    d.init_process_group('gloo', timeout=datetime.timedelta(seconds=5))\n"
+                "except Exception as e:\n"
+                "    print(str(e))\n")
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]), RANK="0",
+                   WORLD_SIZE="2")
+        out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert bench.port_taken(RuntimeError(out.stdout)), out.stdout + out.stderr
+    assert not bench.port_taken(RuntimeError("connection refused"))
+
+
 def test_roofline_steps_per_frame_and_launch():
     """roofline.steps_per_frame is one frame's executed ray-steps of the
     rank's rows, and steps_per_frame x frames_per_launch the launch's (a
