@@ -878,7 +878,9 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
     return (bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
 }
 
-template <class BS>
+// START_WINDOW: d is the orbit's tangent at A (a ray's start, sr_integrate_kernel),
+// so the planar slots may take plane_window_start's directional budget
+template <bool START_WINDOW, class BS>
 __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w,
                                             const float* xneed, const float* xperi, float eo, f3 d, float dphi) {
@@ -926,7 +928,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         if (SR_XCYL && eo <= SR_XCYL_EMAX) xcl |= xcyl_bit(sl, j, xn, xnn, xneed[j - 1]);
         if (SR_XPERI && eo <= xperi[j - 1]) xcl |= 1u << j;
         float e = clearance_obj(sl, A, a) - m0;
-        if (SR_INIT_WINDOW && (sl.type == SR_OBJECT_RECTANGLE || sl.type == SR_OBJECT_DISK ||
+        if (START_WINDOW && SR_INIT_WINDOW && (sl.type == SR_OBJECT_RECTANGLE || sl.type == SR_OBJECT_DISK ||
                                sl.type == SR_OBJECT_HOLLOW_DISK || sl.type == SR_OBJECT_PLANE) &&
             sl.mp < INFINITY && e < 0.5f * a) {
             const float w = plane_window_start(sl, A, d, a, m0, dphi);
@@ -2085,12 +2087,17 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
     SR_PROBE(SR_PROF_CLOCK(prof_bi_));  // budget_init's cycles (section 22)
     if (!CULL) bs.setUhi(INFINITY);
     if (CULL)
-        budget_init(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
-                    fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xlow_need,
-                    fr.xperi_e, orbit_e(r.u, r.du),
-                    // the ray's start (sr_integrate_kernel): r.rd is the orbit's tangent at r.ro;
-                    // a resumed ray's is a chord direction (no start window: NaN gives 0)
-                    RECORD ? r.rd : F3(NAN, NAN, NAN), fr.max_dphi);
+        // the ray's start (sr_integrate_kernel): r.rd is the orbit's tangent at
+        // r.ro; a resumed ray's is a chord direction, so no start window. (Round
+        // 6: the resume passed a NaN direction "to get 0", but fminf drops a NaN
+        // operand, and plane_window_start returned its caps: a window toward a
+        // plane the resumed ray was heading into, missing its hit whenever no
+        // wave-mate's event re-anchored the slot first - three pixels of a
+        // four-frame batch of the stress scene, varying run to run with the
+        // worklist's order, tests/test_gpu_parity.py test_resumed_rays_*.)
+        budget_init<RECORD>(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                            fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xlow_need,
+                            fr.xperi_e, orbit_e(r.u, r.du), r.rd, fr.max_dphi);
     SR_PROBE(FireProbe<Ray, BS> fire_probe_(r, bs));
     const int N = fr.max_steps;
     // every chord is tested exactly when objects outside the budget slots or
@@ -2202,11 +2209,14 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // contains a budgeted cylinder's axis (the usual case, CMV 0) the
         // limit is fixed and there is no direction test; with one, the chord's
         // direction is tested on every step (CMV 1) or, when every lane is in
-        // a black-hole u window, on the first step of each three-step
+        // a black-hole u window, on the first step of each FU-step
         // iteration only (CMV 2, SR_CM_ITER): with u <= uhi < 1 at every
         // applied step's ends the orbit's tangent turns by at most 1.5 u per
-        // radian of phi (dpsi/dphi = 1.5 u^3 / (u^2 + u'^2)), so the next two
-        // chords lie within 4.55 max_dphi of the tested one's direction, below
+        // radian of phi (dpsi/dphi = 1.5 u^3 / (u^2 + u'^2)), and a chord's
+        // direction is the tangent's at a point of its own step, so the next
+        // FU - 1 chords lie within 1.515 FU max_dphi of the tested one's
+        // direction (4.55 max_dphi at three steps; round 6: the bound was
+        // still the three-step one when the loop went to four), below
         // the 0.0555 rad between chord_parallel's threshold (|d_perp|^2 <
         // 2 SR_BUDGET_DPMIN, direction known to 0.004) and the margin's
         // (|d_perp|^2 >= SR_BUDGET_DPMIN). The exit step's chord is tested
@@ -2350,9 +2360,9 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             return u;
         };
         // CMV 2 needs every lane in a u window (u <= uhi < 1 at applied steps)
-        // and the three chords' turning 1.5 x 1.01 x 3 max_dphi within 0.05
+        // and the iteration's chords' turning 1.5 x 1.01 x FU max_dphi within 0.05
         const bool cm_iter = SR_CM_ITER && any_cm && !__ballot(!(uhi < 1.0f)) &&
-                             4.55f * fr.max_dphi < 0.05f;
+                             (1.515f * (float)FU) * fr.max_dphi < 0.05f;
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
@@ -2367,6 +2377,31 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             break;
         }
         SR_PROBE(SR_PROF_BUMP(r.prof, 19, 1));
+        // Past the singularity: u before and after the step both +inf or NaN.
+        // RK4 keeps u there (inf + x is inf or NaN, NaN stays NaN) and no
+        // compare of the loop fires (u < 0, u < u_f, the hole's window), so
+        // the reference runs on to max_steps, and every chord from here has
+        // both ends at +-0 or NaN (point_at divides by u): length 0 or NaN,
+        // direction 0 / 0 or NaN / x, NaN in all three components. Each
+        // primitive test then misses whatever its origin: sphere_test's and
+        // cyl_test's discriminant is NaN (not < 0) and so are their roots
+        // (lam stays -1 / in1, in2 false); plane_test's denominator is NaN
+        // (not < eps) and so is lam (not >= 0), which fails the disks,
+        // rectangles and boxes too. So the ray ends at max_steps with no
+        // further hit and a final direction of three NaNs, whose get_bg
+        // (bilinear's s = t = 0 for any NaN, whatever its sign or payload)
+        // is the loop's: leave the loop for its end (r.i = N; up = r.u makes
+        // settle_prev(N)'s chord one of those). The stress scene's rays
+        // through an object's translucent skin at the shell ran ~1800 such
+        // steps, each an event with every slot tested (round 6: its frame
+        // alone 31.0 -> 4.6 ms). Here, before the slow path proper, the check
+        // left the hot instantiation's allocation as it was; placed after the
+        // degenerate-chord flag or in the event it cost ~0.8 % per frame
+        // (profiles/r06/s20_s31).
+        if (CULL && !(r.u < INFINITY) && !(un < INFINITY)) {
+            up = r.u;
+            break;
+        }
         // ---- slow path of step i
         r.i = i;
         r.steps = sbase + i + 1;
@@ -2385,29 +2420,6 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // length, NaN direction) and the exact tests decide what its NaN
         // arithmetic hits, so every slot is tested (reach below)
         const bool degen = CULL && !(un < 1.0e30f && r.u < 1.0e30f);
-        // Past the singularity: u before and after the step both +inf or NaN.
-        // RK4 keeps u there (inf + x is inf or NaN, NaN stays NaN) and no
-        // compare of the loop fires (u < 0, u < u_f, the hole's window), so
-        // the reference runs on to max_steps, and every chord from here has
-        // both ends at +-0 or NaN (point_at divides by u): length 0 or NaN,
-        // direction 0 / 0 or NaN / x, NaN in all three components. Each
-        // primitive test then misses whatever its origin: sphere_test's and
-        // cyl_test's discriminant is NaN (not < 0) and so are their roots
-        // (lam stays -1 / in1, in2 false); plane_test's denominator is NaN
-        // (not < eps) and so is lam (not >= 0), which fails the disks,
-        // rectangles and boxes too. So the ray ends at max_steps with no
-        // further hit and a final direction of three NaNs, whose get_bg
-        // (bilinear's s = t = 0 for any NaN, whatever its sign or payload)
-        // is the loop's: end it here. The stress scene's rays through an
-        // object's translucent skin at the shell ran ~1800 such steps, each
-        // an event with every slot tested (round 6: its single frame
-        // 31 -> see DESIGN.md §7).
-        if (CULL && !(r.u < INFINITY) && !(un < INFINITY)) {
-            r.i = N;
-            r.steps = sbase + N;
-            r.rd = F3(NAN, NAN, NAN);
-            return ST_BG;
-        }
         const bool event = !(vb < 0.0f) || bhx || (SR_XPLANE && un < 0.5f * fr.u_f) || degen;
         SR_PROBE(SR_TRACE_AT("slow i=%d u=%.9g un=%.9g uhi=%.9g vb=%g force=%d event=%d bhx=%d m=%g\n", i, r.u, un,
                              uhi, vb, (int)force, (int)event, (int)bhx, bm));

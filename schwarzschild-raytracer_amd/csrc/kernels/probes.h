@@ -81,7 +81,8 @@ __device__ unsigned long long sr_prof[SR_PROF_N * (1 << 17)];
 // SR_TRACE (with SR_LANE_MASK, one unmasked pixel): device printf of the
 // slow path's steps, events and hits of the rays that run (post-mortems)
 #ifdef SR_TRACE
-#define SR_TRACE_AT(...) printf(__VA_ARGS__)
+// (inside integrate: I = the integrate kernel's pass, R = sr_resume_kernel's; the thread)
+#define SR_TRACE_AT(fmt, ...) printf("%c%d " fmt, RECORD ? 'I' : 'R', (int)threadIdx.x, __VA_ARGS__)
 #else
 #define SR_TRACE_AT(...)
 #endif

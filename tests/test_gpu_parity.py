@@ -479,6 +479,78 @@ def test_skewed_frames_budgeted(pkg, gpu, oracle, oracle_tex, shear, scale):
         assert np.array_equal(a, b_)
 
 
+def stacked_layers_scene(sc, abi, n_translucent=4, gap=0.5):
+    """n_translucent translucent rectangles and an opaque one behind them,
+    stacked across the default camera's view (z = 10, 10 - gap, ...): every
+    ray logs four translucent hits (the hit log's capacity), stops as ST_MORE
+    and is resumed by sr_resume_kernel a gap before the opaque layer."""
+    import ctypes as C
+
+    s = abi.Scene()
+    abi.load().sr_scene_clear(C.byref(s))
+    for m, col in ((0, (0.02, 0.04, 0.06, 0.3)), (1, (0.9, 0.2, 0.2, 1.0))):
+        M = s.materials[m]
+        for k in range(4):
+            M.color[k] = col[k]
+        M.ambient, M.diffuse, M.specular, M.shininess = 0.2, 0.8, 0.3, 16.0
+        M.texture_index, M.normal_map_index, M.double_sided_normals = -1, -1, 1
+    axes = sc._axes_from((0.0, 0.0, 1.0))  # normal +z, columns x and -y
+    # three disks, then rectangles (three of each primitive at most)
+    for k in range(n_translucent + 1):
+        z = 10.0 - gap * k
+        if k < 3:
+            t, kind, idx = s.disks[k].plane.transform, abi.OBJECT_DISK, k
+            pos = (0.0, 2.0, z)
+            s.disks[k].radius = 12.0
+        else:
+            t, kind, idx = s.rectangles[k - 3].plane.transform, abi.OBJECT_RECTANGLE, k - 3
+            pos = (-8.0, 10.0, z)  # a corner: x in [-8, 8], y in [-6, 10]
+            s.rectangles[k - 3].width = s.rectangles[k - 3].height = 16.0
+        for i in range(3):
+            t.pos[i] = pos[i]
+        for i in range(9):
+            t.axes[i] = axes[i]
+        o = s.objects[k]
+        o.type, o.index, o.material_index = kind, idx, int(k == n_translucent)
+    s.num_objects = n_translucent + 1
+    s.num_lights = 1
+    L = s.lights[0]
+    for i in range(3):
+        L.transform.pos[i] = (0.0, 5.0, 14.0)[i]
+        L.color[i] = 1.0
+    L.intensity, L.attenuation_constant, L.attenuation_linear, L.attenuation_quadratic = 5.0, 1.0, 0.09, 0.032
+    return s
+
+
+def test_resumed_rays_start_without_a_window(pkg, gpu, oracle, oracle_tex):
+    """Rays resumed after a full hit log (sr_resume_kernel) start from a chord
+    end, not from the orbit's tangent, so they get no directional start
+    window (budget_init<false>). Round 6: the resume passed a NaN direction
+    meant to disable the window, but fminf dropped the NaN and the planar
+    slots got the window's caps: the layer right behind the fourth one was
+    skipped unless a wave-mate's event re-anchored it first (three pixels of
+    a four-frame stress batch, varying with the worklist's order). Here every
+    ray resumes 0.5 before an opaque layer: whole frames bit-exact against
+    the oracle, culling on and off identical, at two step counts."""
+    import torch
+
+    sc, abi = pkg.scenes, pkg.abi
+    scene = stacked_layers_scene(sc, abi)
+    cam = abi.default_camera()
+    for N in (1000, 2000):
+        params = abi.default_params(max_steps=N, percent_black=-1.0)
+        g = gpu_debug(gpu, scene, cam, params, 160, 90)
+        o = oracle.render(scene, cam, params, 160, 90, oracle_tex)
+        # the case is the one described: most rays end on the opaque layer
+        assert (o[0][..., 0] > o[0][..., 2]).mean() > 0.5
+        print(compare(g, o, f"stacked layers, {N} steps"))
+        gpu.set_culling(False)
+        f, b, st = gpu.render_debug(cam, params, 160, 90)
+        torch.cuda.synchronize()
+        gpu.set_culling(True)
+        assert np.array_equal(b.cpu().numpy(), g[0]) and np.array_equal(st.cpu().numpy(), g[2])
+
+
 def test_ray_through_singularity(pkg, gpu, oracle, oracle_tex):
     """A ray that passes the r = 1 shell behind an alpha-0 texel (the chord's
     closest hit is the object, so the hole is not hit) falls on to the
