@@ -45,9 +45,15 @@
 // ~ sqrt(eps) * |o - c| (spheres, the black hole).
 #define SR_MU_PLANAR 1.0e-4f
 #define SR_MU_QUADRATIC 2.0e-3f
-// Cylinders: a near-tangent root of the lateral-surface quadratic can leave
-// the accepted point up to ~2 eps S^2 / (r |d_perp|^2) off the surface
-// (DESIGN.md §5); the margin below carries a ~30x safety factor.
+// Cylinders: the lateral-surface quadratic's computed discriminant is the
+// exact one of a radius r' with |r'^2 - r^2| <= ~12 eps (|X|^2 + r^2) for
+// every chord direction (|X| <= |o - pos|: each rounding is a multiple of
+// |d_perp|^2), so an accepted point lies within min(SR_CYL_QMARGIN Sc^2 / r,
+// 2 SR_MU_QUADRATIC (Sc + r)) of the lateral surface, Sc = S + |pos|_1
+// (tests/test_cyl_lateral_margin.py finds at most 1/25
+// of it). Its root error along the chord grows as 1 / |d_perp|^2 (the
+// round-2 margin divided by |d_perp|^2 for that), but moves the point along
+// the surface, not off it.
 #define SR_CYL_QMARGIN 4.0e-6f
 // Budgeted cylinders: chords with |d_perp|^2 < SR_BUDGET_DPMIN are tested per
 // chord; the budget window is capped at SR_BUDGET_TMAX of path so the
@@ -114,9 +120,11 @@ typedef struct {
 // Culling bounds of the curved test ray (geodesic.hip test_ray_hits_culled),
 // after the segments in the same buffer: blocks of SR_TR_BLOCK consecutive
 // segments, then groups of SR_TR_GROUP blocks. A bound is {centre[3], R,
-// cone axis[3], cos alpha, sin alpha, max |pos|_1, always (1: no culling), -}:
-// every segment's may_hit sphere (bc, br) lies within R of the centre, every
-// segment axis within alpha of the cone axis.
+// cone axis[3], cos alpha, sin alpha, max |pos|_1, always (1: no culling),
+// lateral-margin scale}: every segment's accepted points lie within R of the
+// centre and within the scale x lat_margin of its (frame's) lateral surface
+// (sr_api.cpp frame_norms: 1 + 1e-6 for an orthonormal frame); every segment
+// axis within alpha of the cone axis (unused since round 6).
 #define SR_TR_BLOCK 8
 #define SR_TR_GROUP 8
 #define SR_TR_BLOCKS ((SR_MAX_POINTS - 1 + SR_TR_BLOCK - 1) / SR_TR_BLOCK)
@@ -133,6 +141,16 @@ typedef struct {
     int32_t tr_num_groups;
     float tr_radius;
     float tr_extended_length;
+    // the test ray's budget (geodesic.hip clearance_tr, round 6): the farthest
+    // accepted point's distance from the origin bound (every segment's sphere
+    // and the flat cylinder's ends, +inf when unbounded) and the largest
+    // |pos|_1 of its cylinders
+    float tr_far;
+    float tr_pl1;
+    // the flat cylinder's budget: {M^-1 (0, 1, 0) (its accepted points' axis
+    // direction), |M^-1| (0: not budgeted), |M^-1| |M|^2 (the lateral
+    // margin's scale), the axis' rounding over its length, -, -, -, -}
+    float tr_fg[8];
     int32_t num_budget;       // objects of SR_KIND_BUDGET (<= SR_MAX_BUDGET)
     int32_t budget_idx[SR_MAX_OBJECTS];  // their indices in objs[]
     int32_t budget_cyl_mask;  // bit j-1 set: budget slot j is a cylinder
@@ -217,6 +235,10 @@ typedef struct {
     // the scene's budgeted cylinders (popcount of sr_dev_scene.budget_cyl_mask;
     // the small instantiation handles SR_NC_SMALL)
     int32_t num_budget_cyl;
+    // 1: the test ray is visible (sr_dev_scene.tr_visible): the integrate and
+    // resume kernels' test-ray instantiations, which budget it (geodesic.hip
+    // clearance_tr) instead of testing every chord
+    int32_t tr_visible;
     // sqrt(8 (1 - out_dip)), rounded up: at least the step angle (the budget
     // events' directional plane window, geodesic.hip plane_window)
     float max_dphi;

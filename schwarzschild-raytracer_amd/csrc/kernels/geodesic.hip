@@ -198,6 +198,17 @@ __device__ __forceinline__ void consider(Hit& best, bool hit, const f3& p, f3 o,
     }
 }
 
+// The lateral margin of a cylinder test (device_scene.h SR_CYL_QMARGIN, round
+// 6): an accepted point lies within this of the lateral surface for every
+// chord direction, Sc >= S + |pos|_1 of the chord.
+#ifndef SR_REACH_LAT  // slot_reachable's cylinder margin: lat_margin (1) or round 2's over |d_perp|^2 (0;
+                      // conservative too: 1 measured no faster, profiles/r06/s43)
+#define SR_REACH_LAT 0
+#endif
+__device__ __forceinline__ float lat_margin(float Sc, float r) {
+    return fminf(SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r), 2.0f * SR_MU_QUADRATIC * (Sc + r)) * 1.001f;
+}
+
 // Conservative segment culling (not part of the reference; exact by margin):
 // every primitive's accepted hit point lies on the chord [o, o + len*d] up to
 // rounding and inside the object's bounding sphere, so a chord whose distance
@@ -211,13 +222,12 @@ __device__ __forceinline__ bool may_hit(const sr_dev_obj& ob, f3 o, f3 d, float 
     float d2 = dot(q, q);
     float R = ob.br + ob.mu * S;
     if (ob.type == SR_OBJECT_CYLINDER) {
-        // the quadratic's root error grows as S^2 / (r * |d_perp|^2)
-        float ca = dot(d, ld3(ob.f + SR_F_AXES + 3));
-        float dp = 1.0f - ca * ca;
-        float r = ob.f[SR_F_P0 + 1];
-        if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
-        const float Sc = S + ob.pl1;  // the root error scales with |o - pos|
-        R = R + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp);
+        // an accepted point lies within lat_margin of the lateral surface,
+        // whatever the chord's direction (round 6; the root's error along
+        // the chord, S^2 / (r |d_perp|^2), moves it along the surface)
+        const float r = ob.f[SR_F_P0 + 1];
+        if (!(r > 0.0f)) return true;
+        R = R + lat_margin(S + ob.pl1, r);  // |o - pos| <= S + |pos|_1
     }
     return !(d2 > R * R);
 }
@@ -614,14 +624,17 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 // registers (held in VGPRs across it they were spilled to scratch and
 // reloaded at every event). The default scene's kernel (6 slots, 1 cylinder)
 // takes 17 rows, 4.25 KiB per 64-lane wave.
-template <int NB, int NC>
+template <int NB, int NC, bool TR = false>
 struct BudgetLayout {
     static constexpr int PA0 = NB + 1;
     static constexpr int SLAB0 = PA0 + 2 * NC;
     static constexpr int BT = SLAB0 + NC;
     static constexpr int BM = BT + 1, BCX = BT + 2, BCY = BT + 3, BMH = BT + 4, BCM = BT + 5, BUHI = BT + 6;
-    static constexpr int ROWS = BT + 7;
+    static constexpr int BTR = BT + 7;  // the test ray's budget (TR instantiations, clearance_tr)
+    static constexpr int ROWS = BT + 7 + (TR ? 1 : 0);
 };
+// reach bit of the test ray (budget_event, closest_hit_chord)
+#define SR_REACH_TR (1u << 30)
 // The black hole's u window (SR_BH_WINDOW). Every chord of the step loop
 // joins two orbit points at radii 1/u (within 3e-6 relative) and subtends
 // the step's angle dphi at the origin, so it stays in the half-plane beyond
@@ -725,10 +738,11 @@ __device__ __forceinline__ float ball_q(float R, float cx, float cy) {
     return __builtin_fmaf(2.0e-6f * s, s, (cx * cx + cy * cy) - Rt * Rt);
 }
 
-template <int NB_, int NC_>
+template <int NB_, int NC_, bool TR_ = false>
 struct Budget {
-    using L = BudgetLayout<NB_, NC_>;
+    using L = BudgetLayout<NB_, NC_, TR_>;
     static constexpr int NB = NB_, NC = NC_;
+    static constexpr bool TR = TR_;
     float* E;  // &lds[threadIdx.x]: E[j * SR_E_STRIDE], then pa[k], pb[k] (below)
     // Scalars in LDS rows (L::BT ..), read with volatile loads so that no
     // register holds them across the fast loop:
@@ -761,6 +775,8 @@ struct Budget {
     __device__ __forceinline__ void setCm(uint32_t cm, uint32_t excl) const {
         st(L::BCM, __uint_as_float(cm | (excl << 8)));
     }
+    __device__ __forceinline__ float etr() const { return ld(L::BTR); }
+    __device__ __forceinline__ void setEtr(float v) const { st(L::BTR, v); }
     __device__ __forceinline__ float uhi() const { return ld(L::BUHI); }
     __device__ __forceinline__ void setUhi(float v) const { st(L::BUHI, v); }
     // the inner window (uhi in (SR_BH_U, 1): sr_dev_frame.bh_u2 / bh_u3)
@@ -878,10 +894,14 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
     return (bs.cm() >> __builtin_popcount(cyl & ((1u << (j - 1)) - 1u))) & 1u;
 }
 
+__device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs, f3 A, bool outward,
+                              float a, float dip);
+
 // START_WINDOW: d is the orbit's tangent at A (a ray's start, sr_integrate_kernel),
 // so the planar slots may take plane_window_start's directional budget
 template <bool START_WINDOW, class BS>
-__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 nv, f3 tv,
+__device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                            BS& bs, f3 A, f3 nv, f3 tv,
                                             bool outward, float dip, bool bh_ok, bool falling, float xs, float u2w,
                                             const float* xneed, const float* xperi, float eo, f3 d, float dphi) {
     const float a = __builtin_amdgcn_sqrtf(dot(A, A));
@@ -913,6 +933,11 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         if (outward && outward_clear(1.0f, 0.0f, SR_MU_QUADRATIC, 0.0f, 0.0f, a, dip)) e = INFINITY;
         e -= m0;
         bs.E[0] = e;
+        m = nmin(m, e);
+    }
+    if constexpr (BS::TR) {  // the test ray (clearance_tr)
+        const float e = clearance_tr(sc, segs, A, outward, a, dip) - m0;
+        bs.setEtr(e);
         m = nmin(m, e);
     }
     // One pass over the slots; slot j + 1's record is loaded while slot j
@@ -959,7 +984,7 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
 // read from LDS once per fast loop: they change only at reseeds.
 template <int NC>
 struct CylDirs {
-    float pa[NC], pb[NC];
+    float pa[NC > 0 ? NC : 1], pb[NC > 0 ? NC : 1];
 };
 template <class BS>
 __device__ __forceinline__ CylDirs<BS::NC> cyl_dirs(const sr_dev_scene* __restrict__ sc, const BS& bs) {
@@ -1059,12 +1084,17 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
             }
         }
         if (sl.type == SR_OBJECT_CYLINDER) {
+            const float r = sl.x1;
+#if SR_REACH_LAT  // the lateral margin for every chord direction (lat_margin, round 6)
+            if (!(r > 0.0f)) return true;
+            R = R + lat_margin(S + sl.pl1, r);
+#else
             const float ca = dot(dv, ld3(sl.a1));
             const float dp = (dd - ca * ca) * __builtin_amdgcn_rcpf(dd) * 0.5f;
-            const float r = sl.x1;
             if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
             const float Sc = S + sl.pl1;
             R = R + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp);
+#endif
         }
     }
     R = R * 1.001f + perr;
@@ -1090,7 +1120,8 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // slots some lane has spent - usually one - run their clearance and reach
 // tests; all lanes re-anchor those.
 template <class BS>
-__device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, BS& bs, f3 A, f3 B,
+__device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
+                                                 BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
                                                  bool falling, bool par_recompute, float u_f, float u2, float u3,
@@ -1100,7 +1131,7 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     const int nb = sc->num_budget;
     const uint32_t cyl = (uint32_t)sc->budget_cyl_mask;  // budget index (slot - 1) of each budgeted cylinder
     const float T = bs.T();
-    float e[NS], h[NC];
+    float e[NS], h[NC > 0 ? NC : 1];
 #pragma unroll
     for (int j = 0; j < NS; j++) e[j] = bs.E[j * SR_E_STRIDE];
     {
@@ -1198,6 +1229,24 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
     // the spent ones re-anchor at B
     const float a = __builtin_amdgcn_sqrtf(dot(B, B));
     uint32_t reach = 0;
+    if constexpr (BS::TR) {  // the test ray's budget: spent (or a new frame) re-anchors it for every lane
+        const float et = bs.etr();
+        if (__ballot(!(T + ahead < et)) || __ballot(reanchor_cyl)) {
+            const bool h = reanchor_cyl || !(T < et);  // this lane's budget did not cover the chord
+            const float v = clearance_tr(sc, segs, B, outward, a, dip) - perr;
+            bs.setEtr(v);
+            m = nmin(m, v);
+            SR_STAT(22, 1);  // (the small instantiation's counter of slot 8, which it lacks)
+            if (__ballot(h)) {
+                reach |= SR_REACH_TR;
+                SR_STAT(10, 1);
+            }
+        } else {
+            const float v = et - T;
+            bs.setEtr(v);
+            m = nmin(m, v);
+        }
+    }
     const uint32_t xcl = SR_XPLANE ? bs.excl() : 0u;  // slots off this orbit's plane (budget_frame)
     for (uint32_t w = spent; w; w &= w - 1) {
         const int j = __builtin_ctz(w);
@@ -1295,32 +1344,24 @@ __device__ __forceinline__ void test_ray_hits(const sr_dev_scene* __restrict__ s
 
 // Culled test-ray hits for one exact chord [o, o + seg d] of the step loop
 // (frag:760-803: the flat cylinder, then every curved segment). A segment is
-// skipped only when the chord stays beyond the reach may_hit would give a
-// budgeted cylinder of its pose (bounding sphere + mu S + the quadratic's
-// root-error margin SR_CYL_QMARGIN Sc^2 / (r |d_perp|^2)), the rule that culls
-// the scene's own cylinders; decided for a whole block or group of segments
-// at once (sr_api.cpp test_ray_bounds: every segment's sphere lies within R
-// of the bound's centre, its axis within alpha of the cone axis, so |d_perp|^2
-// >= 1 - cos^2(phi - alpha) for a chord at angle phi from the cone axis). The
-// survivors are the exhaustive loop's tests with the same keys, so the
-// winner is the same.
+// skipped only when the chord stays beyond the reach of its accepted points:
+// its bounding sphere (as may_hit's for a cylinder of that pose) grown by mu
+// S and the lateral margin lat_margin (round 6: for every chord direction;
+// round 5 divided the quadratic's margin by |d_perp|^2 and tested every
+// segment of a block whose cone of axes held a chord's direction); decided
+// for a whole block or group of segments at once (sr_api.cpp
+// test_ray_bounds: every segment's sphere lies within R of the bound's
+// centre). The survivors are the exhaustive loop's tests with the same keys,
+// so the winner is the same.
 __device__ __forceinline__ bool tr_bound_may_hit(const float* __restrict__ B, f3 o, f3 d, float seg, float S, float r) {
-    if (B[10] != 0.0f) return true;  // a segment without a proven bound
+    if (B[10] != 0.0f || !(r > 0.0f)) return true;  // a segment without a proven bound
     const f3 w = ld3(B) - o;
     float t = dot(w, d);
     t = t < 0.0f ? 0.0f : t;
     t = t > seg ? seg : t;
     const f3 q = w - d * t;
     const float d2 = dot(q, q);
-    const float cphi = fabsf(dot(d, ld3(B + 4)));
-    const float cosa = B[7], sina = B[8];
-    // max over the block of |d . a1_k| <= cos(phi - alpha) for phi > alpha
-    const float sphi = __builtin_amdgcn_sqrtf(fmaxf(0.0f, 1.0f - cphi * cphi));
-    const float maxc = cphi >= cosa ? 1.0f : fminf(1.0f, __builtin_fmaf(cphi, cosa, sphi * sina) * 1.00001f + 1.0e-6f);
-    const float dp = 1.0f - maxc * maxc;
-    if (!(dp > 1.0e-6f) || !(r > 0.0f)) return true;
-    const float Sc = S + B[9];
-    const float R = (B[3] + SR_MU_PLANAR * S + SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r * dp)) * 1.001f;
+    const float R = (B[3] + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + B[9], r) * B[11];
     return !(d2 > R * R);
 }
 __device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
@@ -1354,6 +1395,77 @@ __device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restr
     }
 }
 
+// The test ray's budget (round 6; the test-ray instantiations, TR): a
+// lane's clearance from every test-ray cylinder, for the chords of a ball
+// around the anchor A as the budget slots' (clearance_obj), so that a chord
+// inside the lane's ball needs no test-ray test at all; before it, every
+// chord of every ray was exact and tested while the overlay was visible
+// (frag:760-803 in every step of frag:890-933). An accepted point of a
+// cylinder test lies on the chord, within lat_margin of the lateral surface
+// for every chord direction and within its height slab up to mu S: within
+// a block's or group's bound radius of its centre (test_ray_bounds), or of
+// the flat cylinder's axis segment by its radius, grown by those margins.
+// For chords in a ball of radius W <= the clearance around A, S <= |A|_1 +
+// 4 W + 1 (clearance_obj), W capped at SR_BUDGET_TMAX. Groups closer than
+// SR_TR_REFINE take the better of their own bound and their blocks'.
+#ifndef SR_TR_REFINE
+#define SR_TR_REFINE 2.0f
+#endif
+__device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 A, float l1A, float r) {
+    const f3 w = A - ld3(B);
+    const float dist = __builtin_amdgcn_sqrtf(dot(w, w));
+    const float d0 = dist - B[3];
+    const float W = fminf(fmaxf(d0, 0.0f), SR_BUDGET_TMAX);
+    const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
+    const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + B[9], r) * B[11] + 3.0e-5f * dist;
+    return B[10] != 0.0f ? -INFINITY : d0 - m;
+}
+__device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs, f3 A, bool outward,
+                              float a, float dip) {
+    const float r = sc->tr_radius;
+    if (!(r > 0.0f)) return -INFINITY;
+    // outward lanes (outward_clear's premises and S bound) beyond every accepted point
+    if (outward) {
+        const float S = __builtin_fmaf(0.01f * a, a, __builtin_fmaf(2.0f, a, 1.0f));
+        if (a * dip > (sc->tr_far + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + sc->tr_pl1, r)) return INFINITY;
+    }
+    const float l1A = fabsf(A.x) + fabsf(A.y) + fabsf(A.z);
+    float e;
+    {  // the flat cylinder: within |M^-1| r (+ margins) of [pos, pos + length g] (sr_dev_scene.tr_fg)
+        const float* t = sc->tr_flat;
+        const float* fg = sc->tr_fg;
+        const f3 w = A - ld3(t);
+        const f3 g = ld3(fg);
+        // the closest point of the axis segment, as a parameter in [0, length] (g . g within 1e-5 of 1)
+        float h = dot(w, g) * __builtin_amdgcn_rcpf(dot(g, g));
+        h = h > 0.0f ? h : 0.0f;
+        h = h < t[12] ? h : t[12];
+        const f3 q = w - g * h;
+        const float d0 = __builtin_amdgcn_sqrtf(dot(q, q)) - r * fg[3];
+        const float W = fminf(fmaxf(d0, 0.0f), SR_BUDGET_TMAX);
+        const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
+        const float pl1 = fabsf(t[0]) + fabsf(t[1]) + fabsf(t[2]);
+        const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + pl1, r) * fg[4] + fg[5] +
+                        3.0e-5f * (fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + t[12]);
+        e = fg[3] > 0.0f ? d0 - m : -INFINITY;
+    }
+    const float* blocks = segs + (SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
+    const float* groups = blocks + SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
+    const int nb = sc->tr_num_blocks, ng = sc->tr_num_groups;
+    for (int g = 0; g < ng; g++) {
+        float eg = tr_clear_bound(groups + g * SR_TR_BOUND_FLOATS, A, l1A, r);
+        if (__ballot(eg < SR_TR_REFINE)) {
+            float eb = INFINITY;
+            const int b1 = min(nb, (g + 1) * SR_TR_GROUP);
+            for (int b = g * SR_TR_GROUP; b < b1; b++)
+                eb = nmin(eb, tr_clear_bound(blocks + b * SR_TR_BOUND_FLOATS, A, l1A, r));
+            eg = eb > eg ? eb : eg;  // both bound the group's segments; NaN eg stays NaN
+        }
+        e = nmin(e, eg);
+    }
+    return nmin(e, SR_BUDGET_TMAX);
+}
+
 // intersect(), frag:755-814, exhaustively: the closest hit along
 // [o, o + max_lambda*d] (max_lambda < 0: unbounded).
 __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
@@ -1373,10 +1485,13 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 // winner as closest_hit_all (lexicographic keys, skipped tests provably
 // miss). One copy of each exact test: candidates go into a wave-uniform
 // object mask first.
+// TR: the test rays are tested only when the test ray's budget may be reached
+// (SR_REACH_TR; elsewhere every chord tests them)
+template <bool TR = false>
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                                  uint32_t reach, f3 o, f3 d, float seg) {
     Hit best = no_hit();
-    test_ray_hits_culled(sc, segs, best, o, d, seg);
+    if (!TR || (reach & SR_REACH_TR)) test_ray_hits_culled(sc, segs, best, o, d, seg);
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
@@ -2076,11 +2191,11 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 __shared__ int sr_lds_ev[SR_WG / 64];
 
 template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL,
-          int NC = SR_MAX_CYLINDERS>
+          int NC = SR_MAX_CYLINDERS, bool TR = false>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
-    using BS = Budget<NB, NC>;
+    using BS = Budget<NB, NC, TR && CULL>;
     __shared__ float lds_E[BS::L::ROWS * SR_E_STRIDE];  // blockDim.x == SR_E_STRIDE
     BS bs;
     bs.E = lds_E + threadIdx.x;
@@ -2095,14 +2210,15 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // wave-mate's event re-anchored the slot first - three pixels of a
         // four-frame batch of the stress scene, varying run to run with the
         // worklist's order, tests/test_gpu_parity.py test_resumed_rays_*.)
-        budget_init<RECORD>(sc, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+        budget_init<RECORD>(sc, segs, bs, r.ro, r.nv, r.tv, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                             fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, fr.xplane_s, fr.bh_u2, fr.xlow_need,
                             fr.xperi_e, orbit_e(r.u, r.du), r.rd, fr.max_dphi);
     SR_PROBE(FireProbe<Ray, BS> fire_probe_(r, bs));
     const int N = fr.max_steps;
     // every chord is tested exactly when objects outside the budget slots or
-    // the test rays are present (wave-uniform)
-    const bool every = !CULL || sc->num_step > 0 || sc->tr_visible;
+    // the test rays are present (wave-uniform); the test-ray instantiations
+    // budget the test rays (clearance_tr)
+    const bool every = !CULL || sc->num_step > 0 || (sc->tr_visible && !BS::TR);
     // Chord bookkeeping: im = the step whose chord r.ro / r.rd hold; up = u
     // after step i - 2 (outside the fast loop: it leaves `up` behind and
     // recover_up() recomputes it); rA ~ 1 / u after step i - 1. r.steps =
@@ -2198,7 +2314,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         // some lane's orbital plane nearly contains a budgeted cylinder's axis
         // (bs.cm changes only at reseeds, outside the fast loop)
         const uint32_t bcm = CULL ? bs.cm() : 0u;
-        const bool any_cm = CULL && __ballot(bcm != 0u);
+        // (an instantiation without budgeted cylinders, NC = 0, has no such lane)
+        const bool any_cm = CULL && NC > 0 && __ballot(bcm != 0u);
         // {step_size, step_size / 6, cos phi, sin phi}, {g, 0.5 step_size, K_i, -},
         // read through the constant address space: scalar loads
         const sr_cfloat4* tp = (const sr_cfloat4*)(tbl + i);
@@ -2366,10 +2483,15 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         using I0 = std::integral_constant<int, 0>;
         using I1 = std::integral_constant<int, 1>;
         using I2 = std::integral_constant<int, 2>;
-        if (cm_iter) fast(I2{});
-        else if (any_cm) fast(I1{});
-        else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
-        else fast(I0{});
+        if constexpr (NC > 0) {
+            if (cm_iter) fast(I2{});
+            else if (any_cm) fast(I1{});
+            else if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
+            else fast(I0{});
+        } else {
+            if (CULL && SR_COAST && !__ballot(!(lim0 == INFINITY))) coast();
+            else fast(I0{});
+        }
         SR_PT(0);
         if (i >= N) {
             SR_PROBE(SR_STAT_STEPHIST(56, N - 1 - ick); SR_STAT_STEPHIST(57, 1));  // recover_up's replayed steps
@@ -2487,10 +2609,10 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_PT(2);
                 // the inner window's bound for this lane: steep falling lanes get bh_u3
                 const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
-                reach = budget_event(sc, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                reach = budget_event(sc, segs, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
                                      fr.u_f, fr.bh_u2, fr.bh_u3, steep);
-                if (__ballot(degen)) reach |= (2u << sc->num_budget) - 1u;
+                if (__ballot(degen)) reach |= ((2u << sc->num_budget) - 1u) | SR_REACH_TR;
                 SR_PT(6);
                 SR_PROBE(probe_reach(r, reach));
                 SR_PROBE(SR_TRACE_AT("  event reach=%x uhi'=%.9g m'=%g E0=%g\n", reach, bs.uhi(), bs.m(), bs.ld(0)));
@@ -2505,7 +2627,8 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             f3 delta = r.ro - prev;
             float seg = len(delta);
             r.rd = delta / seg;
-            hit = CULL ? closest_hit_chord(sc, segs, reach, prev, r.rd, seg) : closest_hit_all(sc, segs, prev, r.rd, seg);
+            hit = CULL ? closest_hit_chord<BS::TR>(sc, segs, reach, prev, r.rd, seg)
+                       : closest_hit_all(sc, segs, prev, r.rd, seg);
             SR_PT(4);
             SR_PROBE(SR_TRACE_AT("  chord i=%d seg=%g slot=%d\n", i, seg, hit.slot));
             if (hit.slot != SLOT_NONE) {
@@ -2578,8 +2701,8 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 // budgeted cylinders of the small instantiation: its cylinder loops (phase 1,
 // chord_parallel in the cylinder-plane fast loop) run over one, and its LDS
 // layout holds 17 rows instead of 25 (no VGPR spills left in it)
-#ifndef SR_NC_SMALL
-#define SR_NC_SMALL 1
+#ifndef SR_NC_SMALL  // round 6: 0 (no budgeted cylinder needs the direction tests, sr_api.cpp SR_CYL_DIRFREE)
+#define SR_NC_SMALL 0
 #endif
 #ifndef SR_GENERAL_WAVES_PER_EU
 #define SR_GENERAL_WAVES_PER_EU 5
@@ -2637,7 +2760,9 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // sr_launch_geodesic picks SR_NB_SMALL when it suffices: the default scene
 // has six, and phase 1 of an event runs over every slot of the capacity).
 // NC: budgeted cylinders it handles (SR_NC_SMALL with SR_NB_SMALL).
-template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS>
+// TR: the test-ray instantiation (the test ray budgeted, clearance_tr)
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS,
+          bool TR = false>
 __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
     const uint32_t* __restrict__ arr, const uint8_t* __restrict__ opq, sr_dev_frame fr, float* __restrict__ ps_base,
@@ -2681,7 +2806,7 @@ __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrat
         Hit hit;
         int st = init_pixel(fr, fr.cam[frame], q, r);
         SR_PROBE(st = wp.lane_mask(q.px, q.py, fr.width, st, ST_DONE); wp.ray_start(r));
-        if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC>(sc, segs, tbl, fr, tx, r, hit, log);
+        if (st < 0) st = integrate<CULL, true, WCOST, NB, FU, NC, TR>(sc, segs, tbl, fr, tx, r, hit, log);
         const size_t id = log.id();
         ps.put_rec(id, ps_word(st, log.n, r.steps), r.rd);
         SR_PROBE(wp.pixel(st, log.n));
@@ -2879,7 +3004,7 @@ __global__ __launch_bounds__(256, SR_SHADE_WAVES_PER_EU) void sr_shade_kernel(co
     write_pixel(fr, out, pitch, dbg_rgba, dbg_steps, q, frag, steps_at);
 }
 
-template <bool CULL>
+template <bool CULL, bool TR = false>
 __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __restrict__ sc,
                                                        const float4* __restrict__ tbl,
                                                        const float* __restrict__ segs,
@@ -2914,7 +3039,8 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         HitLog log{ps, 0};  // RECORD = false: nothing is logged
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();
-            const int st = integrate<CULL, false>(sc, segs, tbl, fr, tx, r, hit, log);
+            const int st = integrate<CULL, false, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_MAX_CYLINDERS, TR>(
+                sc, segs, tbl, fr, tx, r, hit, log);
             if (st == ST_HIT) {
                 f4 c = shade(sc, fr, tx, hit, -r.rd);
                 frag = frag + c;
@@ -2957,6 +3083,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     // scene fits it, the general one (8 slots) or the large one (every object)
     const bool small = cull && fr->num_budget <= SR_NB_SMALL && fr->num_budget_cyl <= SR_NC_SMALL;
     const bool general = fr->num_budget <= SR_NB_GENERAL;
+    const bool tr = cull && fr->tr_visible != 0;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (fr->wave_cost && general)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true, SR_NB_GENERAL, SR_FAST_UNROLL, SR_NC_GENERAL>),
@@ -2965,6 +3092,18 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     else if (fr->wave_cost)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true>), dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream,
                            sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
+    else if (small && tr)  // the test-ray instantiations (the overlay visible)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, SR_FAST_UNROLL, SR_NC_SMALL, true>),
+                           dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps,
+                           ps_n, count, order, cost);
+    else if (cull && general && tr)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_GENERAL, SR_FAST_UNROLL, SR_NC_GENERAL, true>),
+                           dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps,
+                           ps_n, count, order, cost);
+    else if (cull && tr)
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_MAX_CYLINDERS, true>),
+                           dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps,
+                           ps_n, count, order, cost);
     else if (small && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)
         hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_NB_SMALL, 2, SR_NC_SMALL>), dim3(slots * B * SR_WG_PER_TILE),
                            dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps, ps_n, count, order, cost);
@@ -2991,7 +3130,10 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
 #define SR_RESUME_TILES 1024u
 #endif
     unsigned nb = (nblocks * B < SR_RESUME_TILES ? nblocks * B : SR_RESUME_TILES) * SR_WG_PER_TILE;
-    if (cull)
+    if (tr)
+        hipLaunchKernelGGL((sr_resume_kernel<true, true>), dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr,
+                           ps, ps_n, out, pitch, dbg_rgba, dbg_steps, list, count);
+    else if (cull)
         hipLaunchKernelGGL(sr_resume_kernel<true>, dim3(nb), dim3(SR_WG), 0, stream, sc, tbl, segs, bg, arr, *fr, ps, ps_n,
                            out, pitch, dbg_rgba, dbg_steps, list, count);
     else

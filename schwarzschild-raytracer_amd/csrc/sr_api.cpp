@@ -19,6 +19,13 @@
 #include "device_scene.h"
 #include "sr/sr.h"
 
+// Round 6: budgeted cylinders take the lateral margin SR_CYL_QMARGIN Sc^2 / r
+// for every chord direction (0: the round-2 margin over SR_BUDGET_DPMIN, and
+// the kernel's direction tests and slab budgets for nearly parallel chords)
+#ifndef SR_CYL_DIRFREE
+#define SR_CYL_DIRFREE 1
+#endif
+
 extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* tbl, const float* segs,
                                          const uint32_t* bg, const uint32_t* arr, const uint8_t* opq,
                                          const sr_dev_frame* fr,
@@ -384,6 +391,49 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
     }
 }
 
+// The spectral norms of M (rows a0, a1, a2) and of M^-1, and M^-1 itself
+// (binary64): the extreme eigenvalues of M M^T in closed form (symmetric
+// 3x3). False for a singular, ill-conditioned (|M| |M^-1| >= 1e3) or
+// non-finite frame. A cylinder test in this frame accepts points q - pos =
+// M^-1 (x, y, z) with x^2 + z^2 within the lateral margin of r^2 and y in
+// its height slab (geodesic.hip lat_margin: the analysis holds in the
+// frame's coordinates), so |M^-1| scales its radius and |M^-1| |M|^2 its
+// lateral margin in world distances.
+bool frame_norms(V3 a0, V3 a1, V3 a2, double& nm, double& ninv, double inv[3][3]) {
+    const double m[3][3] = {{a0.x, a0.y, a0.z}, {a1.x, a1.y, a1.z}, {a2.x, a2.y, a2.z}};
+    double g[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) g[i][j] = m[i][0] * m[j][0] + m[i][1] * m[j][1] + m[i][2] * m[j][2];
+    const double p1 = g[0][1] * g[0][1] + g[0][2] * g[0][2] + g[1][2] * g[1][2];
+    const double q = (g[0][0] + g[1][1] + g[2][2]) / 3.0;
+    double emax = q, emin = q;
+    const double p2 = (g[0][0] - q) * (g[0][0] - q) + (g[1][1] - q) * (g[1][1] - q) + (g[2][2] - q) * (g[2][2] - q) + 2.0 * p1;
+    if (p2 > 0.0) {
+        const double p = std::sqrt(p2 / 6.0);
+        double b[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) b[i][j] = (g[i][j] - (i == j ? q : 0.0)) / p;
+        double r = 0.5 * (b[0][0] * (b[1][1] * b[2][2] - b[1][2] * b[2][1]) - b[0][1] * (b[1][0] * b[2][2] - b[1][2] * b[2][0]) +
+                          b[0][2] * (b[1][0] * b[2][1] - b[1][1] * b[2][0]));
+        r = std::min(1.0, std::max(-1.0, r));
+        const double phi = std::acos(r) / 3.0;
+        emax = q + 2.0 * p * std::cos(phi);
+        emin = q + 2.0 * p * std::cos(phi + 2.0 * 3.14159265358979323846 / 3.0);
+    }
+    const double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                       m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    if (!std::isfinite(det) || det == 0.0 || !(emin > 0.0) || !std::isfinite(emax)) return false;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            const int i1 = (j + 1) % 3, i2 = (j + 2) % 3, j1 = (i + 1) % 3, j2 = (i + 2) % 3;
+            inv[i][j] = (m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1]) / det;  // adjugate / det
+        }
+    // a relative allowance for the closed form's rounding
+    nm = std::sqrt(emax) * (1.0 + 1e-9);
+    ninv = 1.0 / std::sqrt(emin) * (1.0 + 1e-9);
+    return nm * ninv < 1e3;
+}
+
 // Culling bounds of the curved test ray's segments (device_scene.h
 // SR_TR_BLOCK / SR_TR_GROUP; geodesic.hip test_ray_hits_culled). Per segment
 // k the sphere may_hit would use for a budgeted cylinder of that pose (set_bound:
@@ -394,7 +444,7 @@ int pack_object(const sr_scene& s, int i, sr_dev_obj& o) {
 // make their block and group `always` (no culling).
 void test_ray_bounds(float* buf, int nseg, float r, int& nblocks, int& ngroups) {
     struct Seg {
-        double bc[3], br, ax[3], pl1;
+        double bc[3], br, ax[3], pl1, ls;
         bool ok;
     };
     std::vector<Seg> sg((size_t)nseg);
@@ -403,14 +453,20 @@ void test_ray_bounds(float* buf, int nseg, float r, int& nblocks, int& ngroups) 
         Seg& q = sg[(size_t)k];
         const V3 a0 = ld(g + 3), a1 = ld(g + 6), a2 = ld(g + 9);
         const float h = g[12];
-        q.ok = orthonormal(a0, a1, a2) && h >= 0.f && r > 0.f && std::isfinite(h) && std::isfinite(r);
-        const V3 bc = add(ld(g), scl(a1, 0.5f * h));
-        const double R = std::sqrt((double)r * r + 0.25 * (double)h * h);
-        q.bc[0] = bc.x, q.bc[1] = bc.y, q.bc[2] = bc.z;
+        // round 6: any well-conditioned frame (the reference's gram_schmidt of
+        // d.xzy, d, d.zxy leaves some segments' frames ~1e-2 off orthonormal,
+        // which made their blocks test every chord): the sphere of M^-1's
+        // image of the frame's cylinder, its lateral margin scaled (ls)
+        double nm = 1, ninv = 1, inv[3][3];
+        q.ok = frame_norms(a0, a1, a2, nm, ninv, inv) && h >= 0.f && r > 0.f && std::isfinite(h) && std::isfinite(r);
+        const double hh = 0.5 * (double)h;
+        for (int i = 0; i < 3; i++) q.bc[i] = (double)g[i] + inv[i][1] * hh;  // pos + M^-1 (0, h / 2, 0)
+        const double R = ninv * std::sqrt((double)r * r + hh * hh);
         q.br = (R + 1e-4 * (1.0 + std::fabs(q.bc[0]) + std::fabs(q.bc[1]) + std::fabs(q.bc[2]) + R)) * (1.0 + 1e-6);
         q.ax[0] = a1.x, q.ax[1] = a1.y, q.ax[2] = a1.z;
         q.pl1 = std::fabs((double)g[0]) + std::fabs((double)g[1]) + std::fabs((double)g[2]);
-        q.ok = q.ok && std::isfinite(q.br) && std::isfinite(q.pl1);
+        q.ls = ninv * nm * nm * (1.0 + 1e-6);
+        q.ok = q.ok && std::isfinite(q.br) && std::isfinite(q.pl1) && std::isfinite(q.ls);
     }
     // bound of segments [k0, k1) into out[SR_TR_BOUND_FLOATS]
     auto bound = [&](int k0, int k1, float* out) {
@@ -424,13 +480,14 @@ void test_ray_bounds(float* buf, int nseg, float r, int& nblocks, int& ngroups) 
             }
         }
         const double cn = std::sqrt(ca[0] * ca[0] + ca[1] * ca[1] + ca[2] * ca[2]);
-        double Rb = 0.0, cosa = 1.0, pl1 = 0.0;
+        double Rb = 0.0, cosa = 1.0, pl1 = 0.0, ls = 1.0;
         for (int k = k0; k < k1 && ok && cn > 0.0; k++) {
             const Seg& q = sg[(size_t)k];
             const double dx = q.bc[0] - c[0], dy = q.bc[1] - c[1], dz = q.bc[2] - c[2];
             Rb = std::max(Rb, std::sqrt(dx * dx + dy * dy + dz * dz) + q.br);
             cosa = std::min(cosa, (q.ax[0] * ca[0] + q.ax[1] * ca[1] + q.ax[2] * ca[2]) / cn);
             pl1 = std::max(pl1, q.pl1);
+            ls = std::max(ls, q.ls);
         }
         cosa -= 1e-6;  // the float axes and the kernel's dot products
         ok = ok && cn > 0.0 && cosa > 0.0 && std::isfinite(Rb);
@@ -445,7 +502,7 @@ void test_ray_bounds(float* buf, int nseg, float r, int& nblocks, int& ngroups) 
         out[8] = ok ? (float)std::min(1.0, std::sqrt(std::max(0.0, 1.0 - cosa * cosa)) + 1e-6) : 1.f;
         out[9] = (float)(pl1 * (1.0 + 1e-6));
         out[10] = ok ? 0.f : 1.f;
-        out[11] = 0.f;
+        out[11] = ok ? std::nextafter((float)ls, INFINITY) : 1.f;  // the lateral margin's scale (>= 1)
     };
     float* blocks = buf + (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
     float* groups = blocks + (size_t)SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
@@ -901,6 +958,7 @@ int launch(sr_ctx* ctx, const sr_camera* cams, int n_frames, const sr_params* pa
     // the black hole's u window (geodesic.hip SR_BH_WINDOW): chord origins within r = 100
     fr.num_budget = ctx->h_scene.num_budget;
     fr.num_budget_cyl = __builtin_popcount((unsigned)ctx->h_scene.budget_cyl_mask);
+    fr.tr_visible = ctx->h_scene.tr_visible ? 1 : 0;
     fr.win_ok = fr.uf_radius <= 100.0f;
     {  // the low-energy exclusions (xlow_need, xperi_e), per (u_f, step angle)
         if (!(ctx->xc_uf == fr.u_f && ctx->xc_dphi == fr.max_dphi)) {
@@ -1221,8 +1279,11 @@ static void pack_slot(const sr_dev_obj& o, int cyl, sr_dev_slot& sl) {
         sl.x0 = f[SR_F_P0];
         sl.x1 = f[SR_F_P0 + 1];
         // a margin factor: rounded away from zero so the product bounds the
-        // quotient the margin was specified with
-        const double q = (double)SR_CYL_QMARGIN / ((double)sl.x1 * (double)SR_BUDGET_DPMIN);
+        // quotient the margin was specified with. SR_CYL_DIRFREE: the lateral
+        // margin SR_CYL_QMARGIN Sc^2 / r holds for every chord direction
+        // (tests/test_cyl_lateral_margin.py), so the
+        // direction floor SR_BUDGET_DPMIN no longer divides it
+        const double q = (double)SR_CYL_QMARGIN / ((double)sl.x1 * (SR_CYL_DIRFREE ? 1.0 : (double)SR_BUDGET_DPMIN));
         sl.qk = (float)(q * (1.0 + 1e-5));
         break;
     }
@@ -1250,9 +1311,12 @@ int sr_set_scene(sr_ctx* c, const sr_scene* s) {
         // bounded objects fall back to per-chord bounding-sphere tests
         if (o.kind == SR_KIND_BUDGET && d.num_budget >= SR_MAX_BUDGET) o.kind = SR_KIND_CHORD;
         if (o.kind == SR_KIND_BUDGET) {
-            pack_slot(o, o.type == SR_OBJECT_CYLINDER ? __builtin_popcount((unsigned)d.budget_cyl_mask) : -1,
-                      d.slots[d.num_budget]);
-            if (o.type == SR_OBJECT_CYLINDER) d.budget_cyl_mask |= 1 << d.num_budget;
+            // SR_CYL_DIRFREE: no budgeted cylinder needs the direction tests
+            // (chord_parallel) or the slab budget of chords nearly parallel
+            // to its axis: its distance budget covers every direction
+            const bool dirs = !SR_CYL_DIRFREE && o.type == SR_OBJECT_CYLINDER;
+            pack_slot(o, dirs ? __builtin_popcount((unsigned)d.budget_cyl_mask) : -1, d.slots[d.num_budget]);
+            if (dirs) d.budget_cyl_mask |= 1 << d.num_budget;
             d.budget_idx[d.num_budget++] = i;
         } else {
             d.step_idx[d.num_step++] = i;
@@ -1318,6 +1382,43 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
     }
     d.tr_num_segments = nseg;
     test_ray_bounds(segs.data(), nseg, t->radius, d.tr_num_blocks, d.tr_num_groups);
+    // the test ray's budget (geodesic.hip clearance_tr): the flat cylinder's
+    // accepted points lie within |M^-1| (r + its lateral margin) of the
+    // segment [pos, pos + L M^-1 (0, 1, 0)] (frame_norms); the farthest
+    // accepted point and the largest |pos|_1 for outward lanes
+    {
+        const V3 fp = ld(d.tr_flat), a0 = ld(d.tr_flat + 3), a1 = ld(d.tr_flat + 6), a2 = ld(d.tr_flat + 9);
+        const float L = d.tr_flat[12], r = d.tr_flat[13];
+        double nm = 1, ninv = 1, inv[3][3];
+        bool ok = frame_norms(a0, a1, a2, nm, ninv, inv) && std::isfinite(fp.x) && std::isfinite(fp.y) &&
+                  std::isfinite(fp.z) && L >= 0.f && std::isfinite(L) && r > 0.f && std::isfinite(r);
+        const double g[3] = {inv[0][1], inv[1][1], inv[2][1]};
+        std::memset(d.tr_fg, 0, sizeof d.tr_fg);
+        if (ok) {
+            for (int i = 0; i < 3; i++) d.tr_fg[i] = (float)g[i];
+            // the float axis g's rounding over the length L: radius and margin grown by it
+            const double gerr = 1e-7 * (std::fabs(g[0]) + std::fabs(g[1]) + std::fabs(g[2])) * (double)L;
+            d.tr_fg[3] = std::nextafter((float)(ninv * (1.0 + 1e-6)), INFINITY);
+            d.tr_fg[4] = std::nextafter((float)(ninv * nm * nm * (1.0 + 1e-6)), INFINITY);
+            d.tr_fg[5] = std::nextafter((float)(gerr + 1e-6 * (std::fabs((double)fp.x) + std::fabs((double)fp.y) +
+                                                             std::fabs((double)fp.z))), INFINITY);
+        }
+        const auto n3 = [](double x, double y, double z) { return std::sqrt(x * x + y * y + z * z); };
+        double far = ok ? std::max(n3(fp.x, fp.y, fp.z), n3(fp.x + g[0] * L, fp.y + g[1] * L, fp.z + g[2] * L)) +
+                              ninv * r + (double)d.tr_fg[5]
+                        : INFINITY;
+        double pl1 = std::fabs((double)fp.x) + std::fabs((double)fp.y) + std::fabs((double)fp.z);
+        const float* groups = segs.data() + (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS +
+                              (size_t)SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
+        for (int g = 0; g < d.tr_num_groups; g++) {
+            const float* B = groups + (size_t)g * SR_TR_BOUND_FLOATS;
+            far = B[10] != 0.f ? INFINITY : std::max(far, n3(B[0], B[1], B[2]) + (double)B[3]);
+            pl1 = std::max(pl1, (double)B[9]);
+        }
+        // the float centre's distance and a 1e-5 relative allowance
+        d.tr_far = std::isfinite(far) ? std::nextafter((float)(far * (1.0 + 1e-5) + 1e-5), INFINITY) : INFINITY;
+        d.tr_pl1 = std::nextafter((float)(pl1 * (1.0 + 1e-6)), INFINITY);
+    }
     if (!hip_ok(hipSetDevice(c->device)) || !wait_ctx(c)) return SR_E_HIP;
     if (!hip_ok(hipMemcpyAsync(c->d_segs, segs.data(), segs.size() * sizeof(float), hipMemcpyHostToDevice,
                                c->upload)) ||

@@ -1,0 +1,162 @@
+"""The lateral-surface quadratic's direction-free margin (DESIGN.md §5,
+round 6 "Cylinders: the margin does not depend on the chord's direction").
+
+cyl_test (geodesic.hip; frag:523-571) computes in binary32, in the
+cylinder's local frame, X = (lo.x, lo.z), Y = (ld.x, ld.z):
+    D = (X.Y)^2 + |Y|^2 (r^2 - |X|^2),  lam = -(X.Y +- sqrt D) / |Y|^2.
+Every rounding of D is a multiple of |Y|^2 (|X.Y| <= |X||Y|), so the
+computed D is the exact discriminant of a radius r' with
+|r'^2 - r^2| <= c u (|X|^2 + r^2), c ~ 12, whatever the direction; the
+computed root lies within 4 u (|X| + r') of a root of that radius along
+the line's lateral motion (|dlam| |Y|), so an accepted point p (on the
+chord, within the height slab) lies within
+    min(c u (|X|^2 + r^2) / r,  sqrt(c u (|X|^2 + r^2)))
+of the lateral surface however nearly parallel the chord is to the axis.
+(The root's error *along* the chord grows as 1 / |Y|^2 - that is what the
+round-2 margin SR_CYL_QMARGIN S^2 / (r |d_perp|^2) priced - but it moves
+the point along the surface, not off it.) The budgets use
+    lat(Sc) = min(SR_CYL_QMARGIN Sc^2 / r,  2 SR_MU_QUADRATIC (Sc + r)),
+Sc = |o|_1 + len + 1 + |pos|_1 >= |X| + len.
+
+This test runs the kernel's binary32 expressions (numpy float32, no
+contraction, as hipcc -ffp-contract=off) on adversarial chords - grazing
+lines at every angle to the axis from 1e-7 rad to perpendicular, far and
+near origins, thin and thick tubes - and checks every accepted point's
+binary64 distance from the lateral surface against lat(Sc), with the
+safety factor asserted.
+"""
+import numpy as np
+import pytest
+
+F = np.float32
+QMARGIN = 4.0e-6
+MU_Q = 2.0e-3
+
+
+def gram_schmidt_f32(d):
+    """test_ray_frame / the scene's orthonormal frames: float32 columns c0, c1 = d/|d|, c2."""
+    d = d.astype(F)
+    m0 = np.stack([d[:, 0], d[:, 2], d[:, 1]], 1)
+    m1 = d
+    m2 = np.stack([d[:, 2], d[:, 0], d[:, 1]], 1)
+
+    def dot(a, b):
+        return (a[:, 0] * b[:, 0] + a[:, 1] * b[:, 1]) + a[:, 2] * b[:, 2]
+
+    def proj(v, t):
+        return t * (dot(v, t) / dot(t, t))[:, None]
+
+    m0 = m0 - proj(m0, m1)
+    m2 = (m2 - proj(m2, m1)) - proj(m2, m0)
+    nrm = lambda v: v / np.sqrt(dot(v, v))[:, None]
+    return nrm(m0), nrm(m1), nrm(m2)
+
+
+def orthonormal_f32(a, b, c, tol=1e-5):
+    def dot(x, y):
+        return (x[:, 0] * y[:, 0] + x[:, 1] * y[:, 1]) + x[:, 2] * y[:, 2]
+    ok = np.ones(len(a), bool)
+    for x, y in ((a, a), (b, b), (c, c)):
+        ok &= np.abs(dot(x, y) - F(1)) < tol
+    for x, y in ((a, b), (a, c), (b, c)):
+        ok &= np.abs(dot(x, y)) < tol
+    return ok
+
+
+def cyl_test_f32(o, d, pos, c0, c1, c2, height, radius, max_lambda):
+    """geodesic.hip cyl_test, operation for operation in binary32."""
+    def dot(a, b):
+        return (a[:, 0] * b[:, 0] + a[:, 1] * b[:, 1]) + a[:, 2] * b[:, 2]
+
+    w = o - pos
+    lo = np.stack([dot(c0, w), dot(c1, w), dot(c2, w)], 1)
+    ld = np.stack([dot(c0, d), dot(c1, d), dot(c2, d)], 1)
+    z = F(0) * F(0)
+    opsq = (lo[:, 0] * lo[:, 0] + lo[:, 2] * lo[:, 2]) + z
+    dpsq = (ld[:, 0] * ld[:, 0] + ld[:, 2] * ld[:, 2]) + z
+    a = lo[:, 0] * ld[:, 0] + lo[:, 2] * ld[:, 2]
+    D = a * a + dpsq * (radius * radius - opsq)
+    ok = ~(D < F(0))
+    sq = np.sqrt(np.where(ok, D, F(0)))
+    l1 = -(a + sq) / dpsq
+    l2 = -(a - sq) / dpsq
+    p1 = o + d * l1[:, None]
+    p2 = o + d * l2[:, None]
+    h1 = dot(p1 - pos, c1)
+    h2 = dot(p2 - pos, c1)
+    in1 = (h1 >= 0) & (h1 <= height)
+    in2 = (h2 >= 0) & (h2 <= height)
+    both = in1 & in2
+    lam = np.full_like(l1, F(-1))
+    pos1, pos2 = l1 > 0, l2 > 0
+    lb = np.where(pos1 & pos2, np.minimum(l1, l2), np.where(pos1, l1, np.where(pos2, l2, F(-1))))
+    lam = np.where(both, lb, np.where(in1, l1, np.where(in2, l2, lam)))
+    p = o + d * lam[:, None]
+    hit = ok & (in1 | in2) & (lam >= 0) & (lam <= max_lambda)
+    return hit, p
+
+
+def lateral_dev(p, pos, c1, r):
+    """binary64 distance of p from the lateral surface of radius r about
+    the line pos + t c1 (c1 normalised in binary64)."""
+    a = c1.astype(np.float64)
+    a /= np.linalg.norm(a, axis=1, keepdims=True)
+    w = p.astype(np.float64) - pos.astype(np.float64)
+    t = np.sum(w * a, 1)
+    rho = np.linalg.norm(w - a * t[:, None], axis=1)
+    return np.abs(rho - r.astype(np.float64))
+
+
+def lat_margin(sc, r):
+    return np.minimum(QMARGIN * sc * sc / r, 2.0 * MU_Q * (sc + r))
+
+
+@pytest.mark.parametrize("radius", [0.025, 0.3, 2.0])
+def test_cylinder_hits_stay_on_the_lateral_surface(radius):
+    rng = np.random.default_rng(int(radius * 1000) + 7)
+    n = 400_000
+    # axis and frame
+    ax = rng.normal(size=(n, 3))
+    c0, c1, c2 = gram_schmidt_f32(ax)
+    pos = rng.uniform(-20, 20, size=(n, 3)).astype(F)
+    height = F(1000.0) if radius < 0.1 else F(5.0)
+    r = np.full(n, radius, dtype=F)
+    # chord direction at angle theta from the axis (1e-7 rad .. pi/2)
+    theta = 10.0 ** rng.uniform(-7, np.log10(np.pi / 2), size=n)
+    e1 = c0.astype(np.float64) * np.cos(rng.uniform(0, 2 * np.pi, n))[:, None] + \
+        c2.astype(np.float64) * np.sin(rng.uniform(0, 2 * np.pi, n))[:, None]
+    e1 /= np.linalg.norm(e1, axis=1, keepdims=True)
+    a64 = c1.astype(np.float64)
+    a64 /= np.linalg.norm(a64, axis=1, keepdims=True)
+    sgn = np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    d64 = a64 * (np.cos(theta) * sgn)[:, None] + e1 * np.sin(theta)[:, None]
+    d = (d64 / np.linalg.norm(d64, axis=1, keepdims=True)).astype(F)
+    dn = d.astype(np.float64)
+    # the line's closest approach to the axis: grazing the surface (rho = r (1 +- delta))
+    delta = 10.0 ** rng.uniform(-9, -1, n) * np.where(rng.random(n) < 0.5, -1.0, 1.0)
+    rho = radius * (1.0 + delta)
+    # a lateral unit vector perpendicular to both the axis and the direction's lateral part
+    lat_d = dn - a64 * np.sum(dn * a64, 1)[:, None]
+    perp = np.cross(a64, lat_d)
+    perp /= np.linalg.norm(perp, axis=1, keepdims=True)
+    # tangency (closest-approach) point at height in the slab, then the chord start lam0 before it
+    hgt = rng.uniform(-0.1, 1.1, n) * float(height if height < 100 else 20.0)
+    tp = pos.astype(np.float64) + a64 * hgt[:, None] + perp * rho[:, None]
+    seg = 10.0 ** rng.uniform(-2, np.log10(60.0), n)
+    lam0 = seg * rng.uniform(-0.2, 1.2, n)
+    o = (tp - dn * lam0[:, None]).astype(F)
+    seg32 = seg.astype(F)
+    hit, p = cyl_test_f32(o, d, pos, c0, c1, c2, height, r, seg32)
+    # only orthonormal frames are budgeted or culled (sr_api.cpp orthonormal(),
+    # tolerance 1e-5: the reference's gram_schmidt of d.xzy, d, d.zxy is
+    # ill-conditioned for some axes, and such objects stay exact)
+    hit &= orthonormal_f32(c0, c1, c2)
+    assert hit.sum() > 1000, hit.sum()
+    dev = lateral_dev(p[hit], pos[hit], c1[hit], r[hit])
+    o64, pos64 = o[hit].astype(np.float64), pos[hit].astype(np.float64)
+    sc = np.abs(o64).sum(1) + seg[hit] + 1.0 + np.abs(pos64).sum(1)
+    ratio = dev / lat_margin(sc, radius)
+    # the margin keeps a safety factor of at least 4 over the worst case found
+    assert ratio.max() < 0.25, (ratio.max(), int(np.argmax(ratio)))
+    # near-parallel chords are among the accepted ones (the case the old margin priced by 1 / |d_perp|^2)
+    assert (theta[hit] < 1e-3).sum() > 100

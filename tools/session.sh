@@ -22,7 +22,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${SESSION:-session}
 mkdir -p "$OUT"
-V=$PWD/schwarzschild-raytracer_amd/lib/variants
+V=${SR_VARIANTS:-$PWD/schwarzschild-raytracer_amd/lib/variants}  # lib/variants stays out of the GPU push (.gpurunignore): a session copies what it needs to lib/ab
 DRIVER="bench.py --gpus 1 --steps 20 --warmup 5"
 
 step() {  # name timeout cmd... : logs to $OUT/name.log, stops the session on failure

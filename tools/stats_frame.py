@@ -19,6 +19,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--scene", default="tex")
+    ap.add_argument("--test-ray", action="store_true",
+                    help="the press-R overlay (scenes.test_ray_overlay); counters 22 / 10 of a test-ray "
+                         "instantiation are the test ray's re-anchors / reaches")
     ap.add_argument("--max-steps", type=int, default=2000)
     ap.add_argument("--save", default="", help="write the raw per-wave records (.npy) here")
     ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080], help="render only rows [a, b) (waves alone on the chip)")
@@ -44,6 +47,8 @@ def main():
         r.set_scene(sc.scene_stress())
     else:
         r.set_scene(sc.scene_default(textured=args.scene == "tex"))
+    if args.test_ray:
+        r.set_test_ray(sc.test_ray_overlay())
     r.set_background(sc.skybox(2048, 1024))
     arr, _, _ = sc.default_texture_array()
     r.set_texture_array(arr)
