@@ -598,6 +598,14 @@ __device__ __forceinline__ float nmin(float m, float e) { return __builtin_eleme
 #endif
 #define SR_WG_PER_TILE (256 / SR_WG)
 #define SR_E_STRIDE SR_WG
+// Budgeted cylinders whose nearly parallel chords the kernel handles apart
+// (chord_parallel, slab budgets, the cylinder-plane fast loops) in the
+// general and large instantiations and the resume kernel: none since round 6
+// (sr_api.cpp SR_CYL_DIRFREE: the lateral margin holds for every direction);
+// SR_MAX_CYLINDERS for a host built with SR_CYL_DIRFREE=0
+#ifndef SR_NC_KERNEL
+#define SR_NC_KERNEL 0
+#endif
 #ifndef SR_AHEAD
 #define SR_AHEAD 2.0f
 #endif
@@ -2191,7 +2199,7 @@ __device__ __forceinline__ bool flat_misses(const sr_dev_scene* __restrict__ sc,
 __shared__ int sr_lds_ev[SR_WG / 64];
 
 template <bool CULL, bool RECORD, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL,
-          int NC = SR_MAX_CYLINDERS, bool TR = false>
+          int NC = SR_NC_KERNEL, bool TR = false>
 __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
                                          const float4* __restrict__ tbl, const sr_dev_frame& fr, const Tex& tx,
                                          Ray& r, Hit& hit, HitLog& log) {
@@ -2709,10 +2717,15 @@ __device__ __forceinline__ void write_pixel(const sr_dev_frame& fr, uint8_t* __r
 #endif
 // the general instantiation: 8 slots, 3 cylinders (25 LDS rows); scenes with
 // more budget slots run the large one (every object budgeted: SR_MAX_BUDGET
-// slots, 38 rows, 9.5 KiB of LDS per wave: 16 waves per CU, 4 per SIMD)
+// slots; 29 rows, 7.5 KiB of LDS per wave since round 6: 21 waves per CU)
 #define SR_NB_GENERAL 8
-#define SR_NC_GENERAL SR_MAX_CYLINDERS
-#define SR_LARGE_WAVES_PER_EU 4
+#define SR_NC_GENERAL SR_NC_KERNEL
+// the large instantiation at 5 waves per SIMD since round 6 (96 VGPRs, no
+// spills, 7.5 KiB of LDS per wave once the cylinder rows went: the stress
+// scene 1.832 -> 1.647 ms per frame, profiles/r06/s45/stress)
+#ifndef SR_LARGE_WAVES_PER_EU
+#define SR_LARGE_WAVES_PER_EU 5
+#endif
 
 // Waves per SIMD the integrate kernel is built for: SR_MIN_WAVES_PER_EU (7:
 // 72 VGPRs, since round 6: 1.5 % more frames per second and one frame alone
@@ -2761,7 +2774,7 @@ __device__ __forceinline__ int split_thread(int sub, int tid, int lg) {
 // has six, and phase 1 of an event runs over every slot of the capacity).
 // NC: budgeted cylinders it handles (SR_NC_SMALL with SR_NB_SMALL).
 // TR: the test-ray instantiation (the test ray budgeted, clearance_tr)
-template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_MAX_CYLINDERS,
+template <bool CULL, bool WCOST = false, int NB = SR_MAX_BUDGET, int FU = SR_FAST_UNROLL, int NC = SR_NC_KERNEL,
           bool TR = false>
 __global__ __launch_bounds__(SR_WG, sr_integrate_waves(NB, NC)) void sr_integrate_kernel(
     const sr_dev_scene* __restrict__ sc, const float4* __restrict__ tbl, const float* __restrict__ segs,
@@ -3039,7 +3052,7 @@ __global__ __launch_bounds__(SR_WG) void sr_resume_kernel(const sr_dev_scene* __
         HitLog log{ps, 0};  // RECORD = false: nothing is logged
         for (;;) {  // rounds: integrate to the next hit, shade, resume if not opaque
             Hit hit = no_hit();
-            const int st = integrate<CULL, false, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_MAX_CYLINDERS, TR>(
+            const int st = integrate<CULL, false, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_NC_KERNEL, TR>(
                 sc, segs, tbl, fr, tx, r, hit, log);
             if (st == ST_HIT) {
                 f4 c = shade(sc, fr, tx, hit, -r.rd);
@@ -3084,6 +3097,9 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
     const bool small = cull && fr->num_budget <= SR_NB_SMALL && fr->num_budget_cyl <= SR_NC_SMALL;
     const bool general = fr->num_budget <= SR_NB_GENERAL;
     const bool tr = cull && fr->tr_visible != 0;
+    // cylinders with direction tests beyond what the instantiations handle (a
+    // host built with SR_CYL_DIRFREE=0 against a kernel without them)
+    if (cull && fr->num_budget_cyl > SR_NC_KERNEL && !small) return hipErrorInvalidValue;
     if (ev4) (void)hipEventRecord(ev4[0], stream);
     if (fr->wave_cost && general)
         hipLaunchKernelGGL((sr_integrate_kernel<true, true, SR_NB_GENERAL, SR_FAST_UNROLL, SR_NC_GENERAL>),
@@ -3101,7 +3117,7 @@ extern "C" hipError_t sr_launch_geodesic(const sr_dev_scene* sc, const float4* t
                            dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps,
                            ps_n, count, order, cost);
     else if (cull && tr)
-        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_MAX_CYLINDERS, true>),
+        hipLaunchKernelGGL((sr_integrate_kernel<true, false, SR_MAX_BUDGET, SR_FAST_UNROLL, SR_NC_KERNEL, true>),
                            dim3(slots * B * SR_WG_PER_TILE), dim3(SR_WG), 0, stream, sc, tbl, segs, arr, opq, *fr, ps,
                            ps_n, count, order, cost);
     else if (small && fr->fast_unroll == 2)  // latency mode (sr_set_latency_mode)

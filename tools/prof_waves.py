@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rows", type=int, nargs=2, default=[0, 1080])
     ap.add_argument("--scene", default="tex")
     ap.add_argument("--top", type=int, default=10)
+    ap.add_argument("--test-ray", action="store_true", help="the press-R overlay (scenes.test_ray_overlay)")
     args = ap.parse_args()
     os.environ["SR_LIB"] = str(Path(args.lib).resolve())
     import torch
@@ -39,6 +40,8 @@ def main():
     r = pkg.Renderer(0)
     r.set_scene(sc.scene_black_hole_only() if args.scene == "bh" else sc.scene_stress() if args.scene == "stress"
                 else sc.scene_default(textured=args.scene == "tex"))
+    if args.test_ray:
+        r.set_test_ray(sc.test_ray_overlay())
     r.set_background(sc.skybox(2048, 1024))
     arr, _, _ = sc.default_texture_array()
     r.set_texture_array(arr)
