@@ -903,7 +903,7 @@ __device__ __forceinline__ bool cyl_par_bit(const sr_dev_scene* __restrict__ sc,
 }
 
 __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs, f3 A, bool outward,
-                              float a, float dip);
+                              float a, float dip, float rlen, uint32_t& gm);
 
 // START_WINDOW: d is the orbit's tangent at A (a ray's start, sr_integrate_kernel),
 // so the planar slots may take plane_window_start's directional budget
@@ -944,7 +944,8 @@ __device__ __forceinline__ void budget_init(const sr_dev_scene* __restrict__ sc,
         m = nmin(m, e);
     }
     if constexpr (BS::TR) {  // the test ray (clearance_tr)
-        const float e = clearance_tr(sc, segs, A, outward, a, dip) - m0;
+        uint32_t gm;
+        const float e = clearance_tr(sc, segs, A, outward, a, dip, -1.0f, gm) - m0;
         bs.setEtr(e);
         m = nmin(m, e);
     }
@@ -1129,7 +1130,7 @@ __device__ __forceinline__ bool slot_reachable(const sr_dev_slot* slp, int j, f3
 // tests; all lanes re-anchor those.
 template <class BS>
 __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
-                                                 BS& bs, f3 A, f3 B,
+                                                 uint32_t& trmask, BS& bs, f3 A, f3 B,
                                                  float perr, uint32_t par, bool reanchor_cyl, float ahead,
                                                  bool outward, float dip, float dphi, bool bhx, bool bh_ok,
                                                  bool falling, bool par_recompute, float u_f, float u2, float u3,
@@ -1241,11 +1242,16 @@ __device__ __forceinline__ uint32_t budget_event(const sr_dev_scene* __restrict_
         const float et = bs.etr();
         if (__ballot(!(T + ahead < et)) || __ballot(reanchor_cyl)) {
             const bool h = reanchor_cyl || !(T < et);  // this lane's budget did not cover the chord
-            const float v = clearance_tr(sc, segs, B, outward, a, dip) - perr;
+            // the chord lies within its length (+ the end points' error) of B:
+            // the groups (and the flat cylinder) whose clearance from B
+            // exceeds that cannot be reached by it (trmask, clearance_tr)
+            const f3 dv = B - A;
+            const float rlen = __builtin_fmaf(__builtin_amdgcn_sqrtf(dot(dv, dv)), 1.001f, 2.0f * perr + 1.0e-6f);
+            const float v = clearance_tr(sc, segs, B, outward, a, dip, rlen, trmask) - perr;
             bs.setEtr(v);
             m = nmin(m, v);
             SR_STAT(22, 1);  // (the small instantiation's counter of slot 8, which it lacks)
-            if (__ballot(h)) {
+            if (__ballot(h && trmask != 0u)) {
                 reach |= SR_REACH_TR;
                 SR_STAT(10, 1);
             }
@@ -1372,20 +1378,25 @@ __device__ __forceinline__ bool tr_bound_may_hit(const float* __restrict__ B, f3
     const float R = (B[3] + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + B[9], r) * B[11];
     return !(d2 > R * R);
 }
+// MASK (the test-ray instantiations): gm from the event's clearance_tr, bit g
+// (group g) / bit 31 (the flat cylinder) clear where this chord cannot reach
+// that part; it replaces the groups' per-chord bound tests
+template <bool MASK = false>
 __device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
-                                                     Hit& best, f3 o, f3 d, float seg) {
+                                                     Hit& best, f3 o, f3 d, float seg, uint32_t gm = 0xffffffffu) {
     if (!sc->tr_visible) return;
     f3 p;
     const float* t = sc->tr_flat;
     const m3 A = ldm(t + 3);
-    consider(best, cyl_test(o, d, ld3(t), A, t[12], t[13], seg, p), p, o, SLOT_TR_FLAT, 0, KEY_TR_FLAT);
+    if (!MASK || __ballot((gm >> 31) & 1u))
+        consider(best, cyl_test(o, d, ld3(t), A, t[12], t[13], seg, p), p, o, SLOT_TR_FLAT, 0, KEY_TR_FLAT);
     const float S = (fabsf(o.x) + fabsf(o.y) + fabsf(o.z)) + seg + 1.0f;  // as closest_hit_chord's may_hit
     const float r = sc->tr_radius;
     const float* blocks = segs + (SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
     const float* groups = blocks + SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
     const int ns = sc->tr_num_segments, nb = sc->tr_num_blocks, ng = sc->tr_num_groups;
     for (int g = 0; g < ng; g++) {
-        const bool hg = tr_bound_may_hit(groups + g * SR_TR_BOUND_FLOATS, o, d, seg, S, r);
+        const bool hg = MASK ? (bool)((gm >> g) & 1u) : tr_bound_may_hit(groups + g * SR_TR_BOUND_FLOATS, o, d, seg, S, r);
         if (!__ballot(hg)) continue;
         const int b1 = min(nb, (g + 1) * SR_TR_GROUP);
         for (int b = g * SR_TR_GROUP; b < b1; b++) {
@@ -1428,15 +1439,25 @@ __device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 
     const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + B[9], r) * B[11] + 3.0e-5f * dist;
     return B[10] != 0.0f ? -INFINITY : d0 - m;
 }
+// gm (rlen >= 0): bit g for group g, bit 31 for the flat cylinder, set
+// unless that part's clearance from A exceeds rlen (a chord within rlen of A
+// cannot reach it: the S bound of a ball of radius W >= its clearance holds
+// for it while rlen < SR_BUDGET_TMAX); NaN keeps the bit.
 __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs, f3 A, bool outward,
-                              float a, float dip) {
+                              float a, float dip, float rlen, uint32_t& gm) {
+    gm = 0xffffffffu;
+    if (!(rlen < SR_BUDGET_TMAX)) rlen = INFINITY;
     const float r = sc->tr_radius;
     if (!(r > 0.0f)) return -INFINITY;
     // outward lanes (outward_clear's premises and S bound) beyond every accepted point
     if (outward) {
         const float S = __builtin_fmaf(0.01f * a, a, __builtin_fmaf(2.0f, a, 1.0f));
-        if (a * dip > (sc->tr_far + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + sc->tr_pl1, r)) return INFINITY;
+        if (a * dip > (sc->tr_far + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + sc->tr_pl1, r)) {
+            gm = 0u;
+            return INFINITY;
+        }
     }
+    uint32_t mk = 0u;
     const float l1A = fabsf(A.x) + fabsf(A.y) + fabsf(A.z);
     float e;
     {  // the flat cylinder: within |M^-1| r (+ margins) of [pos, pos + length g] (sr_dev_scene.tr_fg)
@@ -1456,6 +1477,7 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
         const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + pl1, r) * fg[4] + fg[5] +
                         3.0e-5f * (fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + t[12]);
         e = fg[3] > 0.0f ? d0 - m : -INFINITY;
+        mk |= (uint32_t)!(e > rlen) << 31;
     }
     const float* blocks = segs + (SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
     const float* groups = blocks + SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
@@ -1469,8 +1491,10 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
                 eb = nmin(eb, tr_clear_bound(blocks + b * SR_TR_BOUND_FLOATS, A, l1A, r));
             eg = eb > eg ? eb : eg;  // both bound the group's segments; NaN eg stays NaN
         }
+        mk |= (uint32_t)!(eg > rlen) << g;
         e = nmin(e, eg);
     }
+    gm = mk;
     return nmin(e, SR_BUDGET_TMAX);
 }
 
@@ -1497,9 +1521,10 @@ __device__ __forceinline__ Hit closest_hit_all(const sr_dev_scene* __restrict__ 
 // (SR_REACH_TR; elsewhere every chord tests them)
 template <bool TR = false>
 __device__ __forceinline__ Hit closest_hit_chord(const sr_dev_scene* __restrict__ sc, const float* __restrict__ segs,
-                                                 uint32_t reach, f3 o, f3 d, float seg) {
+                                                 uint32_t reach, f3 o, f3 d, float seg, uint32_t trmask = 0xffffffffu) {
     Hit best = no_hit();
-    if (!TR || (reach & SR_REACH_TR)) test_ray_hits_culled(sc, segs, best, o, d, seg);
+    if (!TR) test_ray_hits_culled(sc, segs, best, o, d, seg);
+    else if (reach & SR_REACH_TR) test_ray_hits_culled<true>(sc, segs, best, o, d, seg, trmask);
     uint32_t om = 0;  // objects to test (wave-uniform)
     const int ns = sc->num_step;
     for (int j = 0; j < ns; j++) om |= 1u << sc->step_idx[j];
@@ -2576,6 +2601,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
         do {  // `break`: on to step i + 1
             if (!__ballot(event)) break;
             uint32_t reach = 0xffffffffu;
+            uint32_t trmask = 0xffffffffu;  // test-ray parts this lane's chord may reach (budget_event)
             const f2 p1 = phi_cs(i - 1);
             if (CULL) {
                 // the approximate chord (exact start when materialised)
@@ -2617,10 +2643,13 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
                 SR_PT(2);
                 // the inner window's bound for this lane: steep falling lanes get bh_u3
                 const bool steep = r.du > 0.0f && __builtin_fmaf(r.du, r.du, r.u * r.u * (1.0f - r.u)) >= SR_BH_E_MIN;
-                reach = budget_event(sc, segs, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
+                reach = budget_event(sc, segs, trmask, bs, Ap, Bp, pe, par, reseeded, ahead, r.du < 0.0f && r.u < 0.6f, fr.out_dip,
                                      fr.max_dphi, bhx, fr.win_ok && fr.out_dip > SR_BH_DIP, r.du > 0.0f, cm_iter,
                                      fr.u_f, fr.bh_u2, fr.bh_u3, steep);
-                if (__ballot(degen)) reach |= ((2u << sc->num_budget) - 1u) | SR_REACH_TR;
+                if (__ballot(degen)) {
+                    reach |= ((2u << sc->num_budget) - 1u) | SR_REACH_TR;
+                    trmask = 0xffffffffu;
+                }
                 SR_PT(6);
                 SR_PROBE(probe_reach(r, reach));
                 SR_PROBE(SR_TRACE_AT("  event reach=%x uhi'=%.9g m'=%g E0=%g\n", reach, bs.uhi(), bs.m(), bs.ld(0)));
@@ -2635,7 +2664,7 @@ __device__ __forceinline__ int integrate(const sr_dev_scene* __restrict__ sc, co
             f3 delta = r.ro - prev;
             float seg = len(delta);
             r.rd = delta / seg;
-            hit = CULL ? closest_hit_chord<BS::TR>(sc, segs, reach, prev, r.rd, seg)
+            hit = CULL ? closest_hit_chord<BS::TR>(sc, segs, reach, prev, r.rd, seg, trmask)
                        : closest_hit_all(sc, segs, prev, r.rd, seg);
             SR_PT(4);
             SR_PROBE(SR_TRACE_AT("  chord i=%d seg=%g slot=%d\n", i, seg, hit.slot));
