@@ -149,7 +149,8 @@ typedef struct {
     float tr_pl1;
     // the flat cylinder's budget: {M^-1 (0, 1, 0) (its accepted points' axis
     // direction), |M^-1| (0: not budgeted), |M^-1| |M|^2 (the lateral
-    // margin's scale), the axis' rounding over its length, -, -, -, -}
+    // margin's scale), the axis' rounding over its length, the largest
+    // lateral-margin scale of the flat cylinder and every bound, -}
     float tr_fg[8];
     int32_t num_budget;       // objects of SR_KIND_BUDGET (<= SR_MAX_BUDGET)
     int32_t budget_idx[SR_MAX_OBJECTS];  // their indices in objs[]

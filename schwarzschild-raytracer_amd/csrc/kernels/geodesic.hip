@@ -208,6 +208,19 @@ __device__ __forceinline__ void consider(Hit& best, bool hit, const f3& p, f3 o,
 __device__ __forceinline__ float lat_margin(float Sc, float r) {
     return fminf(SR_CYL_QMARGIN * Sc * Sc * __builtin_amdgcn_rcpf(r), 2.0f * SR_MU_QUADRATIC * (Sc + r)) * 1.001f;
 }
+// The same for a chord of length at most len (round 6, the test rays): an
+// accepted point has frame-lateral distance ~r at a parameter in [0, len], so
+// the chord origin's lateral offset |X| is at most (r + len) (1 + 1e-3), and
+// the discriminant's radius r' obeys |r'^2 - r^2| <= 12 u q, q = (r + len)^2 +
+// r^2; the origin's and the point's own roundings add ~3 u Sc. In the
+// frame's coordinates (world distances: the bound's scale |M^-1| |M|^2).
+// Constants ~8x the derivation's (tests/test_cyl_lateral_margin.py: at most
+// 1/40 of this).
+__device__ __forceinline__ float lat_margin_len(float len, float Sc, float r) {
+    const float rl = r + len;
+    const float q = __builtin_fmaf(rl, rl, r * r);
+    return (fminf(6.0e-6f * q * __builtin_amdgcn_rcpf(r), 7.0e-3f * __builtin_amdgcn_sqrtf(q)) + 2.0e-6f * Sc) * 1.001f;
+}
 
 // Conservative segment culling (not part of the reference; exact by margin):
 // every primitive's accepted hit point lies on the chord [o, o + len*d] up to
@@ -1375,7 +1388,7 @@ __device__ __forceinline__ bool tr_bound_may_hit(const float* __restrict__ B, f3
     t = t > seg ? seg : t;
     const f3 q = w - d * t;
     const float d2 = dot(q, q);
-    const float R = (B[3] + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + B[9], r) * B[11];
+    const float R = (B[3] + SR_MU_PLANAR * S) * 1.001f + lat_margin_len(seg, S + B[9], r) * B[11];
     return !(d2 > R * R);
 }
 // MASK (the test-ray instantiations): gm from the event's clearance_tr, bit g
@@ -1436,7 +1449,7 @@ __device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 
     const float d0 = dist - B[3];
     const float W = fminf(fmaxf(d0, 0.0f), SR_BUDGET_TMAX);
     const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
-    const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + B[9], r) * B[11] + 3.0e-5f * dist;
+    const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin_len(2.0f * W, Sb + B[9], r) * B[11] + 3.0e-5f * dist;
     return B[10] != 0.0f ? -INFINITY : d0 - m;
 }
 // gm (rlen >= 0): bit g for group g, bit 31 for the flat cylinder, set
@@ -1452,7 +1465,7 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
     // outward lanes (outward_clear's premises and S bound) beyond every accepted point
     if (outward) {
         const float S = __builtin_fmaf(0.01f * a, a, __builtin_fmaf(2.0f, a, 1.0f));
-        if (a * dip > (sc->tr_far + SR_MU_PLANAR * S) * 1.001f + lat_margin(S + sc->tr_pl1, r)) {
+        if (a * dip > (sc->tr_far + SR_MU_PLANAR * S) * 1.001f + lat_margin_len(S, S + sc->tr_pl1, r) * sc->tr_fg[6]) {
             gm = 0u;
             return INFINITY;
         }
@@ -1474,7 +1487,7 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
         const float W = fminf(fmaxf(d0, 0.0f), SR_BUDGET_TMAX);
         const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
         const float pl1 = fabsf(t[0]) + fabsf(t[1]) + fabsf(t[2]);
-        const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin(Sb + pl1, r) * fg[4] + fg[5] +
+        const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin_len(2.0f * W, Sb + pl1, r) * fg[4] + fg[5] +
                         3.0e-5f * (fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + t[12]);
         e = fg[3] > 0.0f ? d0 - m : -INFINITY;
         mk |= (uint32_t)!(e > rlen) << 31;

@@ -1410,11 +1410,14 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
         double pl1 = std::fabs((double)fp.x) + std::fabs((double)fp.y) + std::fabs((double)fp.z);
         const float* groups = segs.data() + (size_t)(SR_MAX_POINTS - 1) * SR_SEG_FLOATS +
                               (size_t)SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
+        float ls = d.tr_fg[4];  // the largest lateral-margin scale (outward lanes)
         for (int g = 0; g < d.tr_num_groups; g++) {
             const float* B = groups + (size_t)g * SR_TR_BOUND_FLOATS;
             far = B[10] != 0.f ? INFINITY : std::max(far, n3(B[0], B[1], B[2]) + (double)B[3]);
             pl1 = std::max(pl1, (double)B[9]);
+            ls = std::max(ls, B[11]);
         }
+        d.tr_fg[6] = ls;
         // the float centre's distance and a 1e-5 relative allowance
         d.tr_far = std::isfinite(far) ? std::nextafter((float)(far * (1.0 + 1e-5) + 1e-5), INFINITY) : INFINITY;
         d.tr_pl1 = std::nextafter((float)(pl1 * (1.0 + 1e-6)), INFINITY);

@@ -18,6 +18,12 @@ the point along the surface, not off it.) The budgets use
     lat(Sc) = min(SR_CYL_QMARGIN Sc^2 / r,  2 SR_MU_QUADRATIC (Sc + r)),
 Sc = |o|_1 + len + 1 + |pos|_1 >= |X| + len.
 
+For a chord of known length len (the test rays' tests, lat_margin_len) the
+accepted point's frame-lateral distance is ~r at a parameter in [0, len], so
+|X| <= (r + len)(1 + 1e-3) and, in the frame's own coordinates,
+    lat_len = min(6e-6 q / r, 7e-3 sqrt(q)) + 2e-6 Sc,  q = (r + len)^2 + r^2
+(~8x the derivation's 12 u q / r, sqrt(12 u q) and 3 u Sc).
+
 This test runs the kernel's binary32 expressions (numpy float32, no
 contraction, as hipcc -ffp-contract=off) on adversarial chords - grazing
 lines at every angle to the axis from 1e-7 rad to perpendicular, far and
@@ -111,6 +117,19 @@ def lat_margin(sc, r):
     return np.minimum(QMARGIN * sc * sc / r, 2.0 * MU_Q * (sc + r))
 
 
+def lat_margin_len(length, sc, r):
+    q = (r + length) ** 2 + r * r
+    return np.minimum(6e-6 * q / r, 7e-3 * np.sqrt(q)) + 2e-6 * sc
+
+
+def frame_lateral_dev(p, pos, c0, c2, r):
+    """binary64 |rho - r| in the float frame's own lateral coordinates."""
+    w = p.astype(np.float64) - pos.astype(np.float64)
+    x = np.sum(w * c0.astype(np.float64), 1)
+    z = np.sum(w * c2.astype(np.float64), 1)
+    return np.abs(np.sqrt(x * x + z * z) - r.astype(np.float64))
+
+
 @pytest.mark.parametrize("radius", [0.025, 0.3, 2.0])
 def test_cylinder_hits_stay_on_the_lateral_surface(radius):
     rng = np.random.default_rng(int(radius * 1000) + 7)
@@ -160,3 +179,8 @@ def test_cylinder_hits_stay_on_the_lateral_surface(radius):
     assert ratio.max() < 0.25, (ratio.max(), int(np.argmax(ratio)))
     # near-parallel chords are among the accepted ones (the case the old margin priced by 1 / |d_perp|^2)
     assert (theta[hit] < 1e-3).sum() > 100
+    # the length-aware form, in the frame's coordinates (the world distance
+    # scales by the bound's |M^-1| |M|^2, sr_api.cpp frame_norms)
+    fdev = frame_lateral_dev(p[hit], pos[hit], c0[hit], c2[hit], r[hit])
+    ratio_len = fdev / lat_margin_len(seg32[hit].astype(np.float64), sc, radius)
+    assert ratio_len.max() < 0.1, (ratio_len.max(), int(np.argmax(ratio_len)))

@@ -595,6 +595,38 @@ def test_test_ray_far_view(pkg, gpu, oracle, oracle_tex):
     gpu.set_test_ray(abi.default_test_ray())
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_test_ray_budget_random(pkg, gpu, oracle, oracle_tex, seed):
+    """The test ray's budget (round 6, clearance_tr and the group mask) against
+    the oracle's exhaustive loop: random press-R polylines seen from their own
+    camera (every ray starts beside the polyline and the flat cylinder, and
+    the pixels near the polyline's image travel along it) and from another
+    random camera. Random directions give some segments the reference's
+    ill-conditioned gram_schmidt frames (frame_norms' skewed bounds)."""
+    sc, abi = pkg.scenes, pkg.abi
+    cam0 = sc.random_camera(900 + seed)
+    fwd = list(cam0.transform.axes[6:9])
+    pts = abi.test_ray_points(list(cam0.transform.pos), fwd, 300 + 100 * seed, 2)[:abi.MAX_POINTS]
+    tr = abi.default_test_ray()
+    tr.visible = 1
+    tr.num_curved_points = len(pts)
+    for i, p in enumerate(pts):
+        tr.curved_points[i][0], tr.curved_points[i][1], tr.curved_points[i][2] = p
+    for k in range(3):
+        tr.flat_origin[k] = cam0.transform.pos[k] + fwd[k]
+        tr.flat_dir[k] = fwd[k]
+    view = cam0 if seed % 2 == 0 else sc.random_camera(950 + seed)
+    scene = sc.scene_default(textured=False)
+    params = abi.default_params(max_steps=500, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, view, params, 96, 54, tr)
+    o = oracle.render(scene, view, params, 96, 54, oracle_tex, tr)
+    compare(g, o, f"test-ray budget, seed {seed}")
+    # the overlay is on screen (flat: green, curved: red; frag:191-192)
+    b = o[0][..., :3]
+    assert (((b == (255, 0, 0)).all(-1)) | ((b == (0, 255, 0)).all(-1))).sum() > 0
+    gpu.set_test_ray(abi.default_test_ray())
+
+
 @pytest.mark.parametrize("name,pos,fwd,fov,textured", [
     ("close to the hole", (0.0, 0.4, 4.0), (0.0, -0.1, -1.0), 90.0, True),
     ("edge-on accretion disk", (9.0, 0.05, 0.0), (-1.0, 0.0, 0.0), 40.0, True),
