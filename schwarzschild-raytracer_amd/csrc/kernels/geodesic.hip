@@ -1443,6 +1443,9 @@ __device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restr
 #ifndef SR_TR_REFINE
 #define SR_TR_REFINE 2.0f
 #endif
+#ifndef SR_TR_SKIP  // round 6: +5 % on the overlay at the headline size (profiles/r06/s51)
+#define SR_TR_SKIP 1
+#endif
 __device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 A, float l1A, float r) {
     const f3 w = A - ld3(B);
     const float dist = __builtin_amdgcn_sqrtf(dot(w, w));
@@ -1495,7 +1498,23 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
     const float* blocks = segs + (SR_MAX_POINTS - 1) * SR_SEG_FLOATS;
     const float* groups = blocks + SR_TR_BLOCKS * SR_TR_BOUND_FLOATS;
     const int nb = sc->tr_num_blocks, ng = sc->tr_num_groups;
+#if SR_TR_SKIP
+    // SR_TR_SKIP: a group whose distance beyond its radius exceeds both this
+    // lane's clearance so far and rlen by the largest margin any part can
+    // take here (W at its cap) can neither lower the clearance nor be reached:
+    // when that holds for every lane the group costs a distance test only
+    const float Smax = l1A + __builtin_fmaf(4.0f, SR_BUDGET_TMAX, 1.0f);
+    const float mmax = SR_MU_PLANAR * 1.001f * Smax + lat_margin_len(2.0f * SR_BUDGET_TMAX, Smax + sc->tr_pl1, r) * sc->tr_fg[6];
+#endif
     for (int g = 0; g < ng; g++) {
+#if SR_TR_SKIP
+        {
+            const float* B = groups + g * SR_TR_BOUND_FLOATS;
+            const f3 w = A - ld3(B);
+            const float lim = (fmaxf(e, rlen) + B[3] + mmax) * 1.0001f;
+            if (!__ballot(!(dot(w, w) > lim * lim && lim > 0.0f && B[10] == 0.0f))) continue;
+        }
+#endif
         float eg = tr_clear_bound(groups + g * SR_TR_BOUND_FLOATS, A, l1A, r);
         if (__ballot(eg < SR_TR_REFINE)) {
             float eb = INFINITY;

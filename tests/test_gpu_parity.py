@@ -627,6 +627,38 @@ def test_test_ray_budget_random(pkg, gpu, oracle, oracle_tex, seed):
     gpu.set_test_ray(abi.default_test_ray())
 
 
+@pytest.mark.parametrize("kind", ["general", "large", "large_translucent"])
+def test_test_ray_budget_instantiations(pkg, gpu, oracle, oracle_tex, kind):
+    """The test-ray instantiations beyond the small one: an 8-object scene
+    (the general 8-slot kernel with the test ray's row) and 21-object scenes
+    (the large kernel), one with translucent materials so that rays stop with
+    their hit log full and the test-ray resume kernel continues them."""
+    sc, abi = pkg.scenes, pkg.abi
+    if kind == "general":
+        scene = sc.scene_random(7, n_objects=8, translucent=False, planes=False)
+    elif kind == "large":
+        scene = sc.scene_stress()
+    else:
+        scene = sc.scene_random(11, n_objects=21, translucent=True, planes=True)
+    cam0 = sc.camera_look((1.0, 3.0, 16.0), (0.18, -0.1, -1.0))
+    fwd = list(cam0.transform.axes[6:9])
+    pts = abi.test_ray_points(list(cam0.transform.pos), fwd, 600, 2)[:abi.MAX_POINTS]
+    tr = abi.default_test_ray()
+    tr.visible = 1
+    tr.num_curved_points = len(pts)
+    for i, p in enumerate(pts):
+        tr.curved_points[i][0], tr.curved_points[i][1], tr.curved_points[i][2] = p
+    for k in range(3):
+        tr.flat_origin[k] = cam0.transform.pos[k] + fwd[k]
+        tr.flat_dir[k] = fwd[k]
+    view = sc.camera_look((0.0, 2.0, 15.0), (0.0, -2.0, -15.0))
+    params = abi.default_params(max_steps=400, percent_black=-1.0)
+    g = gpu_debug(gpu, scene, view, params, 64, 36, tr)
+    o = oracle.render(scene, view, params, 64, 36, oracle_tex, tr)
+    compare(g, o, f"test-ray budget, {kind} instantiation")
+    gpu.set_test_ray(abi.default_test_ray())
+
+
 @pytest.mark.parametrize("name,pos,fwd,fov,textured", [
     ("close to the hole", (0.0, 0.4, 4.0), (0.0, -0.1, -1.0), 90.0, True),
     ("edge-on accretion disk", (9.0, 0.05, 0.0), (-1.0, 0.0, 0.0), 40.0, True),
