@@ -115,7 +115,8 @@ typedef struct {
 // Texture-array opacity bitmap radius (texels), see sr_api.cpp make_opacity_map
 #define SR_OPQ_RADIUS 2
 
-// One test-ray cylinder: pos[3] axes[9] height radius, padded to 16 floats.
+// One test-ray cylinder: pos[3] axes[9] height radius, then 1 when its frame
+// is orthonormal (the budget's segment refinement), padded to 16 floats.
 #define SR_SEG_FLOATS 16
 // Culling bounds of the curved test ray (geodesic.hip test_ray_hits_culled),
 // after the segments in the same buffer: blocks of SR_TR_BLOCK consecutive

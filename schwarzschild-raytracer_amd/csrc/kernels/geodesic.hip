@@ -1446,6 +1446,12 @@ __device__ __forceinline__ void test_ray_hits_culled(const sr_dev_scene* __restr
 #ifndef SR_TR_SKIP  // round 6: +5 % on the overlay at the headline size (profiles/r06/s51)
 #define SR_TR_SKIP 1
 #endif
+// Blocks closer than SR_TR_SEG take the better of their bound and their
+// segments' own capsules (orthonormal frames only: the segment's float frame
+// measures lateral distance within 1e-5 of the true one there)
+#ifndef SR_TR_SEG
+#define SR_TR_SEG 0.5f
+#endif
 __device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 A, float l1A, float r) {
     const f3 w = A - ld3(B);
     const float dist = __builtin_amdgcn_sqrtf(dot(w, w));
@@ -1454,6 +1460,25 @@ __device__ __forceinline__ float tr_clear_bound(const float* __restrict__ B, f3 
     const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
     const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin_len(2.0f * W, Sb + B[9], r) * B[11] + 3.0e-5f * dist;
     return B[10] != 0.0f ? -INFINITY : d0 - m;
+}
+// One segment's capsule (its axis segment [pos, pos + h c1], radius r):
+// -inf unless its frame is orthonormal (q[14], sr_api.cpp); the frame's
+// 1e-5 tolerance moves lateral distances and the axis by at most 1e-5 of
+// them, inside the 3e-5 allowance
+__device__ __forceinline__ float tr_clear_segment(const float* __restrict__ q, f3 A, float l1A, float r) {
+    const f3 w = A - ld3(q);
+    const f3 ax = ld3(q + 6);
+    float t = dot(w, ax);
+    t = t > 0.0f ? t : 0.0f;
+    t = t < q[12] ? t : q[12];
+    const f3 d = w - ax * t;
+    const float d0 = __builtin_amdgcn_sqrtf(dot(d, d)) - r;
+    const float W = fminf(fmaxf(d0, 0.0f), SR_BUDGET_TMAX);
+    const float Sb = l1A + __builtin_fmaf(4.0f, W, 1.0f);
+    const float pl1 = fabsf(q[0]) + fabsf(q[1]) + fabsf(q[2]);
+    const float m = SR_MU_PLANAR * 1.001f * Sb + lat_margin_len(2.0f * W, Sb + pl1, r) * 1.0001f +
+                    3.0e-5f * (fabsf(w.x) + fabsf(w.y) + fabsf(w.z) + q[12] + r);
+    return q[14] != 0.0f ? d0 - m : -INFINITY;
 }
 // gm (rlen >= 0): bit g for group g, bit 31 for the flat cylinder, set
 // unless that part's clearance from A exceeds rlen (a chord within rlen of A
@@ -1519,8 +1544,16 @@ __device__ float clearance_tr(const sr_dev_scene* __restrict__ sc, const float* 
         if (__ballot(eg < SR_TR_REFINE)) {
             float eb = INFINITY;
             const int b1 = min(nb, (g + 1) * SR_TR_GROUP);
-            for (int b = g * SR_TR_GROUP; b < b1; b++)
-                eb = nmin(eb, tr_clear_bound(blocks + b * SR_TR_BOUND_FLOATS, A, l1A, r));
+            for (int b = g * SR_TR_GROUP; b < b1; b++) {
+                float ebb = tr_clear_bound(blocks + b * SR_TR_BOUND_FLOATS, A, l1A, r);
+                if (SR_TR_SEG > 0.0f && __ballot(ebb < SR_TR_SEG)) {
+                    float es = INFINITY;
+                    const int s1 = min(sc->tr_num_segments, (b + 1) * SR_TR_BLOCK);
+                    for (int k = b * SR_TR_BLOCK; k < s1; k++) es = nmin(es, tr_clear_segment(segs + k * SR_SEG_FLOATS, A, l1A, r));
+                    ebb = es > ebb ? es : ebb;  // both bound the block's segments; NaN ebb stays NaN
+                }
+                eb = nmin(eb, ebb);
+            }
             eg = eb > eg ? eb : eg;  // both bound the group's segments; NaN eg stays NaN
         }
         mk |= (uint32_t)!(eg > rlen) << g;

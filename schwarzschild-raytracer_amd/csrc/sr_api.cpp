@@ -1379,6 +1379,9 @@ int sr_set_test_ray(sr_ctx* c, const sr_test_ray* t) {
         test_ray_frame(diff, g + 3);
         g[12] = h;
         g[13] = t->radius;
+        // 1: an orthonormal frame (tolerance 1e-5) whose own capsule bounds its
+        // accepted points (geodesic.hip clearance_tr's segment refinement)
+        g[14] = orthonormal(ld(g + 3), ld(g + 6), ld(g + 9)) && std::isfinite(h) && h >= 0.f ? 1.f : 0.f;
     }
     d.tr_num_segments = nseg;
     test_ray_bounds(segs.data(), nseg, t->radius, d.tr_num_blocks, d.tr_num_groups);
